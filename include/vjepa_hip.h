@@ -1,0 +1,122 @@
+/*
+ * libvjepa_hip.so — C ABI of the MI355X (gfx950) V-JEPA 2 train-step kernels.
+ *
+ * The reference (weipeilun/vjepa2) is pure PyTorch: its hot path has no FFI. Each entry point below
+ * replaces the ATen call(s) named in its comment (reference file:line); the Python host layer
+ * (vjepa2_amd/) binds them with ctypes (INTEGRATION.md shows the binding) behind the reference's
+ * module API (VisionTransformer / VisionTransformerPredictor forward(), app/vjepa train step).
+ *
+ * Conventions
+ *  - All pointers are device pointers unless stated; dims/strides are in ELEMENTS unless *_bytes.
+ *  - bf16 tensors are raw 16-bit storage; f32 is IEEE float.
+ *  - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); every call only enqueues
+ *    work on it: no host sync, no allocation, so every call is graph-capturable.
+ *  - Return 0 on success, else an error code; vj_get_last_error() gives the message (thread-local).
+ *    The library never exits the process and never frees caller memory.
+ *  - Deterministic: no floating-point atomics anywhere (reductions are fixed-order two-level).
+ */
+#ifndef VJEPA_HIP_H
+#define VJEPA_HIP_H
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int vj_version(void);
+int vj_get_last_error(char* buf, size_t n);
+int vj_device_sync(void);
+
+/* GEMM epilogues */
+enum {
+  VJ_EPI_BF16 = 0,      /* C(bf16) = acc + bias                                           */
+  VJ_EPI_F32 = 1,       /* C(f32)  = acc + bias                                           */
+  VJ_EPI_F32_RESID = 2, /* C(f32)  = aux(f32 residual) + acc + bias   (Block residual add) */
+  VJ_EPI_GELU = 3,      /* C(bf16) = pre = acc + bias (optional), C2(bf16) = GELU_erf(pre) */
+  VJ_EPI_GELU_BWD = 4   /* C(bf16) = acc * GELU'(aux bf16 pre-activation)                 */
+};
+
+/* C[m,n] = sum_k A(m,k) B(n,k) (+ epilogue), bf16 operands, f32 accumulate (MFMA 32x32x16).
+ * A(m,k) = a_kmajor ? A[m*lda+k] : A[k*lda+m];  B(n,k) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n].
+ * Replaces nn.Linear forward/backward (modules.py:77-83, 330, 379-381; predictor.py:182, 244) and the
+ * Conv3d tubelet projection as a GEMM over im2col rows (patch_embed.py:42-52). */
+int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor,
+                 int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc, void* C2, long ldc2,
+                 void* stream);
+
+/* Varlen non-causal flash attention, head_dim 32 or 64 (F.scaled_dot_product_attention,
+ * modules.py:367-372 / 411-418). Tokens of `ngroups` groups of equal-length sequences are
+ * concatenated: group g has nseq[g] sequences of len[g] tokens. q/k/v at columns q_off/k_off/v_off
+ * + h*hd of the [T, ld] bf16 buffer; O bf16 [T, ldo] at column h*hd.
+ * stats: f32 [2][H][T]; forward writes stats[0] = logsumexp (natural log) per (head, token). */
+int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o, long ldo,
+                float* stats, float scale, int ngroups, const int* nseq, const int* len, void* stream);
+/* Backward: writes dq/dk/dv (bf16) into dqkv at the same column offsets; uses stats[0] and writes
+ * stats[1] = rowsum(dO * O). Deterministic (separate dK/dV and dQ sweeps, no atomics). */
+int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, const void* o,
+                long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
+                const int* nseq, const int* len, void* stream);
+
+/* LayerNorm (nn.LayerNorm / F.layer_norm, modules.py:556-563, train.py:417): x f32 or bf16, y bf16 or f32,
+ * gamma/beta optional (both or neither); mean/rstd optional outputs. D % 4 == 0, D <= 2048. */
+int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma, const float* beta,
+                     float eps, void* y, int y_f32, long ldy, float* mean, float* rstd, void* stream);
+/* Backward (dy bf16): dres(f32) = (dres_in or 0) + dx; optional bf16 copy of dres; dgamma/dbeta
+ * accumulated (+=) through a workspace of vj_layernorm_bwd_blocks(M)*2*D floats. */
+int vj_layernorm_bwd_blocks(int M);
+int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const float* x, long ldx, const float* mean,
+                     const float* rstd, const float* gamma, const float* dres_in, long ldri, float* dres, long ldr,
+                     void* dres_bf16, long ldrb, float* dgamma, float* dbeta, float* ws, long ws_floats, void* stream);
+
+/* out[n] (+)= sum_m x[m, n]  (bias gradients). ws >= min(128, ceil(M/256)) * N floats. */
+int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate, float* ws,
+                  long ws_floats, void* stream);
+
+/* 3-axis RoPE of q and k, in place (rotate_queries_or_keys, modules.py:26-50, applied at :343-365).
+ * Token id -> (frame, row, col) with tokens_per_frame / tokens_per_row (modules.py:293-324).
+ * ids: int32 [T] or NULL (then id = t % ids_mod). cos/sin tables f32 [pos][half], half = (hd/3)/2.
+ * inverse = 1 applies the transpose (gradient). */
+int vj_rope(int T, int H, int hd, void* qkv, long ld, int q_off, int k_off, const int* ids, int ids_mod,
+            int tokens_per_frame, int tokens_per_row, const float* cos_tab, const float* sin_tab, int half,
+            int inverse, void* stream);
+
+/* Tubelet im2col for the Conv3d patch embedding, gathering only the kept tokens (PatchEmbed3D +
+ * apply_masks, patch_embed.py:49-52, vision_transformer.py:188-192). Row r = sample r/K, token
+ * idx[r] (int64 mask [B,K] flattened) or r%K when idx is NULL. out bf16 [R, C*tub*p*p]. */
+int vj_im2col_tubelet(int R, int K, const long* idx, int B, int C, int Tf, int Hf, int Wf, int tub, int pch,
+                      const float* clip, void* out, void* stream);
+
+/* Bit-exact row moves (apply_masks gather, predictor sort/unsort, predictor.py:194-241):
+ * scatter=0: dst[r] = src[idx[r]];  scatter=1: dst[idx[r]] = src[r]. */
+int vj_gather_rows(int R, int rowbytes, const void* src, long src_ld_bytes, const int* idx, void* dst,
+                   long dst_ld_bytes, int scatter, void* stream);
+/* dst[idx[r]] = vec (mask tokens, predictor.py:194-197). */
+int vj_fill_rows(int R, int D, float* dst, long ldd, const int* idx, const float* vec, void* stream);
+/* dst[r] += table[idx ? idx[r] : r % idx_mod] (sincos pos-embed add, non-RoPE variant). */
+int vj_add_rows(int R, int D, float* dst, long ldd, const float* table, long ldt, const int* idx, int idx_mod,
+                void* stream);
+
+/* Predictor sort indices for one mask pair: stable rank of cat(mx[b], my[b]) (= torch.argsort for
+ * unique ids, predictor.py:210-217; inverse at :240-242). Outputs int32 (see vj_ops.hip). */
+int vj_pred_index(int B, int K, int Kp, const long* mx, const long* my, int row0, int bmod, int N, int* pos,
+                  int* ctx_dst, int* tgt_rows, int* loss_rows, void* stream);
+int vj_ids64to32(long n, const long* in, int* out, void* stream);
+
+/* Fused forward_target normalisation + JEPA loss + dL/dz (train.py:414-435). */
+int vj_jepa_loss(int R, int D, const float* z, long ldz, const float* tgt, long ldt, const int* loss_rows,
+                 const float* gamma, const float* beta, float eps1, float eps2, float loss_exp, int ngroups,
+                 const int* group_rows, void* dz, long lddz, float* row_loss, float* loss_out, void* stream);
+
+/* Optimizer and EMA over flat fp32 arenas (torch.optim.AdamW foreach math, app/vjepa/utils.py:239;
+ * GradScaler inf-skip train.py:446-451; EMA train.py:456-465). p_bf16 / target_bf16: optional
+ * bf16 shadow copies written in the same pass (the next forward's GEMM operands). */
+int vj_check_finite(long n, const float* g, int* found_inf, void* stream);
+int vj_adamw(long n, float* p, const float* g, float* m, float* v, void* p_bf16, float lr, float beta1, float beta2,
+             float eps, float weight_decay, int step, float grad_scale, const int* found_inf, void* stream);
+int vj_ema(long n, float* target, const float* online, float momentum, void* target_bf16, void* stream);
+int vj_cast_bf16(long n, const float* in, void* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VJEPA_HIP_H */

@@ -1,0 +1,259 @@
+"""ORACLE — test infrastructure only. CPU fp32 restatement of the reference V-JEPA 2 train step.
+
+This module restates, in plain PyTorch CPU ops (fp32), the algorithm of weipeilun/vjepa2's hot path
+so that the HIP product (vjepa2_amd/) can be checked against it. It is imported ONLY by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg — never by the product path.
+
+Pinning: every function here is checked against golden fixtures produced by running the reference
+itself (tests/golden/make_golden.py -> tests/golden/*.pt; tests/test_oracle_golden.py), i.e. the
+oracle is "parity pinned" to the reference's own outputs at fp32.
+
+Each function cites the reference file:line it follows (paths relative to the reference root).
+Weights are passed as plain state-dict mappings using the reference's key names.
+"""
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+# ------------------------------------------------------------------------------------------------
+# src/models/utils/modules.py:26-50
+def rotate_queries_or_keys(x, pos):
+    """Quirky 'RoPE' of the reference: sin/cos tiled [t0..t(h-1), t0..t(h-1)], partner = adjacent pair."""
+    D = x.shape[-1]
+    half = D // 2
+    omega = torch.arange(half, dtype=x.dtype)
+    omega /= D / 2.0
+    omega = 1.0 / 10000**omega
+    freq = pos.to(x.dtype)[..., None] * omega  # (..., N, D/2)
+    s = freq.sin()
+    c = freq.cos()
+    s = torch.cat([s, s], dim=-1)
+    c = torch.cat([c, c], dim=-1)
+    y = x.unflatten(-1, (-1, 2))
+    y = torch.stack((-y[..., 1], y[..., 0]), dim=-1).flatten(-2)
+    return x * c + y * s
+
+
+def rope_tables(hd, max_pos):
+    """cos/sin [max_pos, half] of the per-axis angles, computed with the reference's fp32 op order
+    (modules.py:30-39): omega = 1 / 10000 ** (arange(half) / (sw/2)); theta = pos * omega."""
+    sw = 2 * ((hd // 3) // 2)
+    half = sw // 2
+    omega = torch.arange(half, dtype=torch.float32)
+    omega /= sw / 2.0
+    omega = 1.0 / 10000**omega
+    pos = torch.arange(max_pos, dtype=torch.float32)
+    freq = pos[:, None] * omega[None, :]
+    return freq.cos().contiguous(), freq.sin().contiguous()
+
+
+# src/models/utils/modules.py:293-324
+def separate_positions(ids, tokens_per_frame, tokens_per_row):
+    frame = ids // tokens_per_frame
+    rem = ids - tokens_per_frame * frame
+    height = rem // tokens_per_row
+    width = rem - tokens_per_row * height
+    return frame, height, width
+
+
+def apply_rope_qk(q, k, ids, tokens_per_frame, tokens_per_row):
+    """q, k: [B, H, N, hd]; ids: [B, N] or [N] token ids (modules.py:333-365)."""
+    hd = q.shape[-1]
+    sw = 2 * ((hd // 3) // 2)
+    if ids.dim() == 2:
+        ids = ids[:, None, :].expand(-1, q.shape[1], -1)
+    d, h, w = separate_positions(ids, tokens_per_frame, tokens_per_row)
+    outs_q, outs_k = [], []
+    s = 0
+    for pos in (d, h, w):
+        outs_q.append(rotate_queries_or_keys(q[..., s:s + sw], pos))
+        outs_k.append(rotate_queries_or_keys(k[..., s:s + sw], pos))
+        s += sw
+    if s < hd:
+        outs_q.append(q[..., s:])
+        outs_k.append(k[..., s:])
+    return torch.cat(outs_q, -1), torch.cat(outs_k, -1)
+
+
+# ------------------------------------------------------------------------------------------------
+# src/models/utils/modules.py:326-382 (RoPEAttention) and :385-429 (Attention)
+def attention(x, sd, prefix, num_heads, ids=None, tokens_per_frame=None, tokens_per_row=None, use_rope=True):
+    B, N, C = x.shape
+    qkv = F.linear(x, sd[prefix + "qkv.weight"], sd[prefix + "qkv.bias"])
+    qkv = qkv.unflatten(-1, (3, num_heads, -1)).permute(2, 0, 3, 1, 4)
+    q, k, v = qkv[0], qkv[1], qkv[2]
+    if use_rope:
+        if ids is None:
+            ids = torch.arange(N)
+        q, k = apply_rope_qk(q, k, ids, tokens_per_frame, tokens_per_row)
+    o = F.scaled_dot_product_attention(q, k, v)
+    o = o.transpose(1, 2).reshape(B, N, C)
+    return F.linear(o, sd[prefix + "proj.weight"], sd[prefix + "proj.bias"])
+
+
+# src/models/utils/modules.py:556-563 (Block) with MLP :77-83 (GELU exact)
+def block(x, sd, prefix, num_heads, eps=1e-6, **rope_kw):
+    D = x.shape[-1]
+    y = F.layer_norm(x, (D,), sd[prefix + "norm1.weight"], sd[prefix + "norm1.bias"], eps)
+    x = x + attention(y, sd, prefix + "attn.", num_heads, **rope_kw)
+    y = F.layer_norm(x, (D,), sd[prefix + "norm2.weight"], sd[prefix + "norm2.bias"], eps)
+    y = F.gelu(F.linear(y, sd[prefix + "mlp.fc1.weight"], sd[prefix + "mlp.fc1.bias"]))
+    return x + F.linear(y, sd[prefix + "mlp.fc2.weight"], sd[prefix + "mlp.fc2.bias"])
+
+
+# ------------------------------------------------------------------------------------------------
+# src/models/utils/pos_embs.py:9-38, 75-93 (numpy float64)
+def sincos_1d(embed_dim, pos):
+    omega = np.arange(embed_dim // 2, dtype=float)
+    omega /= embed_dim / 2.0
+    omega = 1.0 / 10000**omega
+    out = np.einsum("m,d->md", pos.reshape(-1), omega)
+    return np.concatenate([np.sin(out), np.cos(out)], axis=1)
+
+
+def sincos_3d(embed_dim, grid_size, grid_depth, uniform_power=False):
+    gd = np.arange(grid_depth, dtype=float)
+    gh = np.arange(grid_size, dtype=float)
+    gw = np.arange(grid_size, dtype=float)
+    gh, gd, gw = np.meshgrid(gh, gd, gw)
+    if not uniform_power:
+        hdim = wdim = embed_dim // 4
+        ddim = embed_dim // 2
+    else:
+        hdim = wdim = ddim = int(np.ceil(embed_dim / 6) * 2)
+    e = np.concatenate([sincos_1d(ddim, gd), sincos_1d(hdim, gh), sincos_1d(wdim, gw)], axis=1)
+    return e[:, :embed_dim]
+
+
+# ------------------------------------------------------------------------------------------------
+# src/masks/utils.py:9-21
+def apply_masks(x, masks, concat=True):
+    outs = [torch.gather(x, 1, m.unsqueeze(-1).expand(-1, -1, x.size(-1))) for m in masks]
+    return torch.cat(outs, 0) if concat else outs
+
+
+# src/models/vision_transformer.py:161-213 (video path, optional RoPE / sincos pos-embed)
+def encoder_forward(x, sd, cfg, masks=None, eps=1e-6, final_norm=True):
+    """cfg: dict(patch_size, tubelet_size, num_heads, depth, use_rope). x: [B, 3, T, H, W]."""
+    p, tub = cfg["patch_size"], cfg["tubelet_size"]
+    B, _, T, H, W = x.shape
+    Tp, Hp, Wp = T // tub, H // p, W // p
+    t = F.conv3d(x, sd["patch_embed.proj.weight"], sd["patch_embed.proj.bias"], stride=(tub, p, p))
+    t = t.flatten(2).transpose(1, 2)
+    if not cfg["use_rope"]:
+        t = t + sd["pos_embed"]
+    ids = None
+    if masks is not None:
+        if not isinstance(masks, list):
+            masks = [masks]
+        t = apply_masks(t, masks)
+        ids = torch.cat(masks, 0)
+    kw = dict(ids=ids, tokens_per_frame=Hp * Wp, tokens_per_row=Wp, use_rope=cfg["use_rope"])
+    for i in range(cfg["depth"]):
+        t = block(t, sd, f"blocks.{i}.", cfg["num_heads"], eps=eps, **kw)
+    if final_norm:
+        t = F.layer_norm(t, (t.shape[-1],), sd["norm.weight"], sd["norm.bias"], eps)
+    return t
+
+
+# src/models/predictor.py:166-246 (RoPE or sincos, mask tokens)
+def predictor_forward(z, masks_x, masks_y, sd, cfg, mask_index=1, eps=1e-6):
+    """cfg: dict(num_heads, depth, use_rope, grid_size, num_mask_tokens, num_patches)."""
+    if not isinstance(masks_x, list):
+        masks_x = [masks_x]
+    if not isinstance(masks_y, list):
+        masks_y = [masks_y]
+    B = len(z) // len(masks_x)
+    x = F.linear(z, sd["predictor_embed.weight"], sd["predictor_embed.bias"])
+    _, Nc, Dp = x.shape
+    if not cfg["use_rope"]:
+        x = x + apply_masks(sd["predictor_pos_embed"].repeat(B, 1, 1), masks_x)
+    tok = sd[f"mask_tokens.{mask_index % cfg['num_mask_tokens']}"]
+    pred = apply_masks(tok.repeat(B, cfg["num_patches"], 1), masks_y)
+    if not cfg["use_rope"]:
+        pe = apply_masks(sd["predictor_pos_embed"].repeat(B, 1, 1), masks_y)
+        pe = torch.cat([torch.cat([pe[i * B:(i + 1) * B] for _ in range(len(masks_x))], 0)
+                        for i in range(len(pe) // B)], 0)
+        pred = pred + pe
+    x = x.repeat(len(masks_x), 1, 1)
+    x = torch.cat([x, pred], 1)
+    mx = torch.cat(masks_x, 0)
+    my = torch.cat(masks_y, 0)
+    m = torch.cat([mx, my], 1)
+    order = torch.argsort(m, dim=1)
+    m = torch.gather(m, 1, order)
+    x = torch.gather(x, 1, order[..., None].expand(-1, -1, Dp))
+    g = cfg["grid_size"]
+    kw = dict(ids=m, tokens_per_frame=g * g, tokens_per_row=g, use_rope=cfg["use_rope"])
+    for i in range(cfg["depth"]):
+        x = block(x, sd, f"predictor_blocks.{i}.", cfg["num_heads"], eps=eps, **kw)
+    x = F.layer_norm(x, (Dp,), sd["predictor_norm.weight"], sd["predictor_norm.bias"], eps)
+    rev = torch.argsort(order, dim=1)
+    x = torch.gather(x, 1, rev[..., None].expand(-1, -1, Dp))[:, Nc:]
+    return F.linear(x, sd["predictor_proj.weight"], sd["predictor_proj.bias"])
+
+
+# ------------------------------------------------------------------------------------------------
+# app/vjepa/train.py:414-435
+def jepa_loss(z_list, h, masks_pred, loss_exp=1.0):
+    """z_list: predictor outputs per mask; h: target features [B, N, D] (already layer-normed)."""
+    hs = apply_masks(h, masks_pred, concat=False)
+    loss, n = 0.0, 0
+    for zi, hi in zip(z_list, hs):
+        loss = loss + torch.mean(torch.abs(zi - hi) ** loss_exp) / loss_exp
+        n += 1
+    return loss / n
+
+
+def forward_target(x, sd_target, cfg):
+    """train.py:414-418: target encoder (all tokens) + F.layer_norm (no affine, eps 1e-5)."""
+    h = encoder_forward(x, sd_target, cfg)
+    return F.layer_norm(h, (h.size(-1),))
+
+
+# ------------------------------------------------------------------------------------------------
+# src/utils/schedulers.py:41-93
+class WarmupCosine:
+    def __init__(self, warmup_steps, start_lr, ref_lr, T_max, final_lr=0.0):
+        self.start_lr, self.ref_lr, self.final_lr = start_lr, ref_lr, final_lr
+        self.warmup_steps, self.T_max, self._step = warmup_steps, T_max - warmup_steps, 0.0
+
+    def step(self):
+        self._step += 1
+        if self._step < self.warmup_steps:
+            return self.start_lr + float(self._step) / float(max(1, self.warmup_steps)) * (self.ref_lr - self.start_lr)
+        progress = float(self._step - self.warmup_steps) / float(max(1, self.T_max))
+        return max(self.final_lr,
+                   self.final_lr + (self.ref_lr - self.final_lr) * 0.5 * (1.0 + math.cos(math.pi * progress)))
+
+
+class CosineWD:
+    def __init__(self, ref_wd, T_max, final_wd=0.0):
+        self.ref_wd, self.final_wd, self.T_max, self._step = ref_wd, final_wd, T_max, 0.0
+
+    def step(self):
+        self._step += 1
+        progress = self._step / self.T_max
+        wd = self.final_wd + (self.ref_wd - self.final_wd) * 0.5 * (1.0 + math.cos(math.pi * progress))
+        return max(self.final_wd, wd) if self.final_wd <= self.ref_wd else min(self.final_wd, wd)
+
+
+# torch.optim.AdamW (foreach math) as configured by app/vjepa/utils.py:207-255
+def adamw_step(p, g, m, v, step, lr, wd, beta1=0.9, beta2=0.999, eps=1e-8):
+    p.mul_(1 - lr * wd)
+    m.lerp_(g, 1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    bc1 = 1 - beta1**step
+    bc2 = 1 - beta2**step
+    denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
+    p.addcdiv_(m, denom, value=-(lr / bc1))
+
+
+# app/vjepa/train.py:456-465
+def ema_update(target, online, m):
+    target.mul_(m)
+    target.add_(online, alpha=1 - m)

@@ -1,0 +1,335 @@
+"""GPU parity tests of every HIP kernel against a plain-PyTorch fp32 reference (or the oracle).
+
+Tolerances: bf16 operands with fp32 accumulation are compared to fp32 math on the SAME bf16-rounded
+operands, so only accumulation order and the bf16 rounding of outputs differ:
+  - f32 outputs:  |err| <= 1e-4 * sqrt(K) * scale     - bf16 outputs: 1 bf16 ulp (rtol 2^-7)
+Index/byte kernels (gather/scatter/fill/index build) must be bit-exact.
+"""
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import vjepa_oracle as orc  # noqa: E402
+
+DEV = "cuda"
+
+
+def _close(got, exp, atol, rtol, what):
+    got = got.detach().float().cpu()
+    exp = exp.detach().float().cpu()
+    err = (got - exp).abs()
+    bad = err > atol + rtol * exp.abs()
+    assert not bool(bad.any()), (
+        f"{what}: max abs err {err.max().item():.3e} (atol {atol}, rtol {rtol}), "
+        f"{int(bad.sum())}/{bad.numel()} bad")
+
+
+# ------------------------------------------------------------------------------------------------
+GEMM_SHAPES = [(128, 128, 64), (300, 136, 72), (264, 200, 1000), (1, 8, 8), (520, 384, 1536)]
+
+
+@pytest.mark.parametrize("a_kmajor", [True, False])
+@pytest.mark.parametrize("b_kmajor", [True, False])
+@pytest.mark.parametrize("shape", GEMM_SHAPES)
+def test_gemm_layouts(a_kmajor, b_kmajor, shape):
+    from vjepa2_amd import ops
+
+    M, N, K = shape
+    if not a_kmajor and M % 8:
+        M += 8 - M % 8
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    B = torch.randn(N, K, generator=g).to(DEV).bfloat16()
+    bias = torch.randn(N, generator=g).to(DEV)
+    exp = A.float() @ B.float().t() + bias
+    a_store = A.contiguous() if a_kmajor else A.t().contiguous()
+    b_store = B.contiguous() if b_kmajor else B.t().contiguous()
+    out = torch.empty(M, N, device=DEV)
+    ops.gemm(M, N, K, a_store, a_store.stride(0), a_kmajor, b_store, b_store.stride(0), b_kmajor, ops.EPI_F32,
+             out=out, ldc=N, bias=bias)
+    torch.cuda.synchronize()
+    _close(out, exp, 1e-4 * math.sqrt(K) * 4, 1e-4, f"gemm {shape} ak={a_kmajor} bk={b_kmajor}")
+
+
+def test_gemm_epilogues():
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(0)
+    M, N, K = 333, 256, 192
+    X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
+    b = torch.randn(N, generator=g).to(DEV)
+    ref = X.float() @ W.float().t() + b
+    y = ops.linear_fwd(X, W, b, ops.EPI_BF16)
+    _close(y, ref, 1e-3, 8e-3, "EPI_BF16")
+    resid = torch.randn(M, N, generator=g).to(DEV)
+    y = ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid)
+    _close(y, ref + resid, 2e-4, 1e-5, "EPI_F32_RESID")
+    pre, act = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
+    _close(pre, ref, 1e-3, 8e-3, "EPI_GELU pre")
+    _close(act, torch.nn.functional.gelu(pre.float()), 1e-3, 8e-3, "EPI_GELU act")
+    # GELU backward epilogue: out = (dY W) * gelu'(pre)
+    dY = torch.randn(M, N, generator=g).to(DEV).bfloat16()
+    W2 = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
+    pre2 = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    x = pre2.float().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(dY.float() @ W2.float())
+    got = ops.linear_dgrad(dY, W2, gelu_pre=pre2)
+    _close(got, x.grad, 2e-3, 1e-2, "EPI_GELU_BWD")
+    # wgrad accumulate
+    dw = torch.randn(N, K, generator=g).to(DEV)
+    exp = dw + dY.float().t() @ pre2.float()
+    ops.linear_wgrad(dY, pre2, dw)
+    _close(dw, exp, 2e-4 * math.sqrt(M), 1e-5, "wgrad accumulate")
+
+
+# ------------------------------------------------------------------------------------------------
+def _attn_ref(q, k, v, groups, scale):
+    """q,k,v f32 [T, H, hd] (concatenated sequences) -> O [T,H,hd], lse [H,T]"""
+    outs, lses = [], []
+    t0 = 0
+    for ns, ln in groups:
+        for _ in range(ns):
+            qq, kk, vv = (x[t0:t0 + ln].transpose(0, 1) for x in (q, k, v))
+            s = (qq @ kk.transpose(-1, -2)) * scale
+            lses.append(torch.logsumexp(s, -1))
+            outs.append((torch.softmax(s, -1) @ vv).transpose(0, 1))
+            t0 += ln
+    return torch.cat(outs, 0), torch.cat(lses, 1)
+
+
+@pytest.mark.parametrize("hd,H,groups", [(64, 2, [(3, 70), (2, 130)]), (32, 3, [(2, 257), (1, 5)]),
+                                         (64, 1, [(1, 128)]), (32, 2, [(4, 33)])])
+def test_attention_fwd_bwd(hd, H, groups):
+    from vjepa2_amd import ops
+
+    T = sum(n * l for n, l in groups)
+    D = H * hd
+    g = torch.Generator(device="cpu").manual_seed(hd + T)
+    qkv = torch.randn(T, 3 * D, generator=g).to(DEV).bfloat16()
+    scale = hd ** -0.5
+    o, stats = ops.attn_fwd(qkv, H, hd, groups, scale)
+    q, k, v = (qkv[:, i * D:(i + 1) * D].float().reshape(T, H, hd).requires_grad_(True) for i in range(3))
+    o_ref, lse_ref = _attn_ref(q, k, v, groups, scale)
+    torch.cuda.synchronize()
+    _close(o.reshape(T, H, hd), o_ref, 1e-2, 2e-2, f"attn fwd hd={hd}")
+    _close(stats[0], lse_ref, 2e-3, 1e-4, f"attn lse hd={hd}")
+    do = torch.randn(T, D, generator=g).to(DEV).bfloat16()
+    o_ref.backward(do.float().reshape(T, H, hd))
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, groups, scale)
+    torch.cuda.synchronize()
+    for i, (name, t) in enumerate((("dq", q), ("dk", k), ("dv", v))):
+        _close(dqkv[:, i * D:(i + 1) * D].reshape(T, H, hd), t.grad, 2e-2, 3e-2, f"attn {name} hd={hd}")
+    # determinism
+    dqkv2 = ops.attn_bwd(qkv, o, do, stats, H, hd, groups, scale)
+    assert torch.equal(dqkv, dqkv2)
+
+
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("D", [64, 384, 1024, 1408])
+def test_layernorm(D):
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(D)
+    M = 301
+    x = (3 * torch.randn(M, D, generator=g) + 1).to(DEV)
+    w = torch.randn(D, generator=g).to(DEV)
+    b = torch.randn(D, generator=g).to(DEV)
+    y, mean, rstd = ops.layernorm_fwd(x, w, b, 1e-6, out_dtype=torch.float32)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-6)
+    _close(y, yr, 1e-4, 1e-4, "ln fwd")
+    yb, _, _ = ops.layernorm_fwd(x, w, b, 1e-6)
+    _close(yb, yr, 1e-3, 8e-3, "ln fwd bf16")
+    dy = torch.randn(M, D, generator=g).to(DEV).bfloat16()
+    yr.backward(dy.float())
+    dres_in = torch.randn(M, D, generator=g).to(DEV)
+    dw = torch.zeros(D, device=DEV)
+    db = torch.zeros(D, device=DEV)
+    dres, dres_bf = ops.layernorm_bwd(dy, x, mean, rstd, w, dres_in=dres_in, dweight=dw, dbias=db, want_bf16=True)
+    torch.cuda.synchronize()
+    _close(dres, xr.grad + dres_in, 1e-4, 1e-4, "ln bwd dx")
+    _close(dres_bf, xr.grad + dres_in, 1e-3, 8e-3, "ln bwd dx bf16")
+    _close(dw, wr.grad, 1e-3, 1e-4, "ln bwd dgamma")
+    _close(db, br.grad, 1e-3, 1e-4, "ln bwd dbeta")
+
+
+def test_colsum():
+    from vjepa2_amd import ops
+
+    x = torch.randn(70000, 96, device=DEV).bfloat16()
+    out = torch.ones(96, device=DEV)
+    ops.colsum(x, out, accumulate=True)
+    _close(out, 1 + x.float().sum(0), 5e-3, 1e-4, "colsum")
+
+
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("hd,H", [(64, 2), (32, 3)])
+def test_rope_fwd_bwd(hd, H):
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(hd)
+    T, D = 200, H * hd
+    tpf, tpr = 16, 4  # 4x4 grid, up to 12 frames
+    ids = torch.randint(0, 12 * 16, (T,), generator=g)
+    qkv = torch.randn(T, 3 * D, generator=g).bfloat16()
+    cos_t, sin_t = orc.rope_tables(hd, 16)
+    qkv_d = qkv.to(DEV)
+    ops.rope_(qkv_d, H, hd, 0, D, ids.to(DEV).int(), 0, tpf, tpr, cos_t.to(DEV), sin_t.to(DEV))
+    q = qkv[:, :D].float().reshape(T, H, hd).transpose(0, 1)[None].requires_grad_(True)
+    k = qkv[:, D:2 * D].float().reshape(T, H, hd).transpose(0, 1)[None]
+    qr, kr = orc.apply_rope_qk(q, k, ids[None], tpf, tpr)
+    torch.cuda.synchronize()
+    got = qkv_d.cpu().float()
+    _close(got[:, :D], qr[0].transpose(0, 1).reshape(T, D), 1e-5, 8e-3, "rope q")
+    _close(got[:, D:2 * D], kr[0].transpose(0, 1).reshape(T, D), 1e-5, 8e-3, "rope k")
+    assert torch.equal(got[:, 2 * D:], qkv[:, 2 * D:].float()), "rope touched v"
+    # inverse == transpose (autograd of the oracle map)
+    gq = torch.randn(T, D, generator=g).bfloat16()
+    qr.backward(gq.float().reshape(T, H, hd).transpose(0, 1)[None])
+    buf = torch.zeros(T, 3 * D).bfloat16()
+    buf[:, :D] = gq
+    buf_d = buf.to(DEV)
+    ops.rope_(buf_d, H, hd, 0, D, ids.to(DEV).int(), 0, tpf, tpr, cos_t.to(DEV), sin_t.to(DEV), inverse=True)
+    torch.cuda.synchronize()
+    _close(buf_d.cpu()[:, :D], q.grad[0].transpose(0, 1).reshape(T, D), 1e-5, 8e-3, "rope inverse")
+
+
+# ------------------------------------------------------------------------------------------------
+def test_im2col_patch_embed():
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(5)
+    B, C, Tf, Hf, Wf, p, tub, D = 2, 3, 4, 32, 48, 16, 2, 64
+    clip = torch.randn(B, C, Tf, Hf, Wf, generator=g)
+    w = 0.05 * torch.randn(D, C, tub, p, p, generator=g)
+    b = torch.randn(D, generator=g)
+    N = (Tf // tub) * (Hf // p) * (Wf // p)
+    mask = torch.stack([torch.randperm(N, generator=g)[:5].sort().values for _ in range(B)])
+    clip_d = clip.to(DEV)
+    cols = ops.im2col(clip_d, p, tub, idx=mask.to(DEV))
+    y = ops.linear_fwd(cols, w.reshape(D, -1).to(DEV).bfloat16(), b.to(DEV), ops.EPI_F32)
+    ref = torch.nn.functional.conv3d(clip.bfloat16().float(), w.bfloat16().float(), b, stride=(tub, p, p))
+    ref = orc.apply_masks(ref.flatten(2).transpose(1, 2), [mask]).reshape(B * 5, D)
+    torch.cuda.synchronize()
+    _close(y.cpu(), ref, 1e-3, 1e-4, "patch embed (masked)")
+    cols_all = ops.im2col(clip_d, p, tub)
+    assert cols_all.shape == (B * N, C * tub * p * p)
+
+
+def test_row_ops_bit_exact():
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(9)
+    src = torch.randn(100, 96, generator=g).to(DEV)
+    idx = torch.randint(0, 100, (37,), generator=g).to(DEV).int()
+    got = ops.gather_rows(src, idx)
+    assert torch.equal(got, src[idx.long()])
+    srcb = src.bfloat16()
+    assert torch.equal(ops.gather_rows(srcb, idx), srcb[idx.long()])
+    perm = torch.randperm(100, generator=g).to(DEV).int()
+    out = torch.zeros_like(src)
+    ops.scatter_rows(src, perm, out)
+    exp = torch.zeros_like(src)
+    exp[perm.long()] = src
+    assert torch.equal(out, exp)
+    vec = torch.randn(96, generator=g).to(DEV)
+    ops.fill_rows(out, perm[:10], vec)
+    exp[perm[:10].long()] = vec
+    assert torch.equal(out, exp)
+
+
+def test_pred_index_matches_argsort():
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    B, N, K, Kp = 4, 2048, 513, 966
+    perms = [torch.randperm(N, generator=g) for _ in range(B)]
+    mx = torch.stack([p[:K].sort().values for p in perms])
+    my = torch.stack([p[K:K + Kp].sort().values for p in perms])
+    n = K + Kp
+    row0 = 17
+    pos = torch.full((row0 + B * n,), -1, dtype=torch.int32, device=DEV)
+    ctx = torch.empty(B * K, dtype=torch.int32, device=DEV)
+    tgt = torch.empty(B * Kp, dtype=torch.int32, device=DEV)
+    lrows = torch.empty(B * Kp, dtype=torch.int32, device=DEV)
+    ops.pred_index(mx.to(DEV), my.to(DEV), row0, N, pos, ctx, tgt, lrows)
+    m = torch.cat([mx, my], 1)
+    order = torch.argsort(m, dim=1)
+    sorted_ids = torch.gather(m, 1, order)
+    rev = torch.argsort(order, dim=1)
+    base = (row0 + torch.arange(B) * n)[:, None]
+    torch.cuda.synchronize()
+    assert torch.equal(pos[row0:].cpu().long().reshape(B, n), sorted_ids)
+    assert torch.equal(ctx.cpu().long().reshape(B, K), base + rev[:, :K])
+    assert torch.equal(tgt.cpu().long().reshape(B, Kp), base + rev[:, K:])
+    assert torch.equal(lrows.cpu().long().reshape(B, Kp), torch.arange(B)[:, None] * N + my)
+
+
+# ------------------------------------------------------------------------------------------------
+def test_jepa_loss():
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(4)
+    B, N, D = 3, 40, 128
+    h_res = torch.randn(B * N, D, generator=g)
+    gamma = 1 + 0.1 * torch.randn(D, generator=g)
+    beta = 0.1 * torch.randn(D, generator=g)
+    masks = [torch.stack([torch.randperm(N, generator=g)[:k].sort().values for _ in range(B)]) for k in (7, 11)]
+    rows = torch.cat([(torch.arange(B)[:, None] * N + m).reshape(-1) for m in masks]).int()
+    z = torch.randn(rows.numel(), D, generator=g)
+    loss, dz, _ = ops.jepa_loss(z.to(DEV), h_res.to(DEV), rows.to(DEV), gamma.to(DEV), beta.to(DEV),
+                                [B * 7, B * 11])
+    h = torch.nn.functional.layer_norm(h_res, (D,), gamma, beta, 1e-6)
+    h = torch.nn.functional.layer_norm(h, (D,)).reshape(B, N, D)
+    zr = z.clone().requires_grad_(True)
+    zl = [zr[:B * 7].reshape(B, 7, D), zr[B * 7:].reshape(B, 11, D)]
+    ref = orc.jepa_loss(zl, h, masks)
+    ref.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - ref.item()) < 1e-5 * max(1.0, ref.item())
+    _close(dz, zr.grad, 1e-9, 8e-3, "loss dz")
+
+
+def test_adamw_ema_match_oracle():
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(6)
+    n = 4096
+    p = torch.randn(n, generator=g)
+    gr = torch.randn(n, generator=g)
+    m = 0.1 * torch.randn(n, generator=g)
+    v = torch.rand(n, generator=g)
+    pd, gd, md, vd = (t.clone().to(DEV) for t in (p, gr, m, v))
+    pbf = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    for step in (1, 2, 3):
+        ops.adamw(pd, gd, md, vd, pbf, 5e-4, 0.9, 0.999, 1e-8, 0.04, step)
+        orc.adamw_step(p, gr, m, v, step, 5e-4, 0.04)
+    torch.cuda.synchronize()
+    _close(pd, p, 1e-7, 1e-6, "adamw p")
+    _close(md, m, 1e-7, 1e-6, "adamw m")
+    _close(vd, v, 1e-7, 1e-6, "adamw v")
+    assert torch.equal(pbf, pd.bfloat16())
+    # found_inf skip
+    flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+    gd[5] = float("inf")
+    ops.check_finite(gd, flag)
+    before = pd.clone()
+    ops.adamw(pd, gd, md, vd, pbf, 5e-4, 0.9, 0.999, 1e-8, 0.04, 4, found_inf=flag)
+    torch.cuda.synchronize()
+    assert flag.item() == 1 and torch.equal(pd, before)
+    t = torch.randn(n, generator=g)
+    e = torch.randn(n, generator=g)
+    td = t.to(DEV)
+    tbf = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    ops.ema(td, e.to(DEV), 0.99925, tbf)
+    orc.ema_update(t, e, 0.99925)
+    torch.cuda.synchronize()
+    _close(td, t, 1e-7, 1e-6, "ema")
+    assert torch.equal(tbf, td.bfloat16())

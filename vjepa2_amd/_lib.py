@@ -1,0 +1,83 @@
+"""ctypes binding of libvjepa_hip.so (include/vjepa_hip.h).
+
+The product path has no CPU fallback: if the library is missing or a call fails, a RuntimeError
+is raised. PyTorch is imported first so that its HIP runtime (libamdhip64.so.7) is the one the
+library binds to.
+"""
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime our library links against)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvjepa_hip.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+
+# name -> argtypes (restype is always int)
+SIGNATURES = {
+    "vj_version": [],
+    "vj_get_last_error": [ctypes.c_char_p, ctypes.c_size_t],
+    "vj_device_sync": [],
+    "vj_gemm_bf16": [_I, _I, _I, _P, _L, _I, _P, _L, _I, _I, _P, _P, _L, _P, _L, _P, _L, _P],
+    "vj_attn_fwd": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _F, _I, _P, _P, _P],
+    "vj_attn_bwd": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _F, _I, _P, _P, _P],
+    "vj_layernorm_fwd": [_I, _I, _P, _I, _L, _P, _P, _F, _P, _I, _L, _P, _P, _P],
+    "vj_layernorm_bwd_blocks": [_I],
+    "vj_layernorm_bwd": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _L, _P, _P, _P, _L, _P],
+    "vj_colsum_f32": [_I, _I, _P, _I, _L, _P, _I, _P, _L, _P],
+    "vj_rope": [_I, _I, _I, _P, _L, _I, _I, _P, _I, _I, _I, _P, _P, _I, _I, _P],
+    "vj_im2col_tubelet": [_I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
+    "vj_gather_rows": [_I, _I, _P, _L, _P, _P, _L, _I, _P],
+    "vj_fill_rows": [_I, _I, _P, _L, _P, _P, _P],
+    "vj_add_rows": [_I, _I, _P, _L, _P, _L, _P, _I, _P],
+    "vj_pred_index": [_I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P],
+    "vj_ids64to32": [_L, _P, _P, _P],
+    "vj_jepa_loss": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _F, _F, _F, _I, _P, _P, _L, _P, _P, _P],
+    "vj_check_finite": [_L, _P, _P, _P],
+    "vj_adamw": [_L, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, _P, _P],
+    "vj_ema": [_L, _P, _P, _F, _P, _P],
+    "vj_cast_bf16": [_L, _P, _P, _P],
+}
+
+_lib = None
+
+
+def load():
+    """Load and type the library (raises if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} not found: the HIP extension is not built (run `python -m vjepa2_amd.build` or "
+            "__graft_entry__.build()). There is no CPU fallback."
+        )
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(1024)
+    load().vj_get_last_error(buf, 1024)
+    return buf.value.decode(errors="replace")
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed (code {rc}): {last_error()}")
+    return rc
+
+
+def int_array(vals):
+    vals = list(vals)
+    return (ctypes.c_int * max(1, len(vals)))(*vals)

@@ -1,0 +1,71 @@
+"""Build libvjepa_hip.so (gfx950) in-tree with hipcc.
+
+The library links against the HIP runtime that PyTorch-ROCm already loads (torch/lib/libamdhip64.so,
+soname libamdhip64.so.7) so one runtime serves torch's streams and our launches.
+
+    python -m vjepa2_amd.build        # or __graft_entry__.build()
+"""
+
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libvjepa_hip.so")
+SOURCES = ["vj_capi.hip", "vj_gemm.hip", "vj_attn.hip", "vj_ops.hip"]
+ARCH = os.environ.get("VJEPA_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-mcode-object-version=5",
+          "-Wno-unused-command-line-argument"]
+
+
+def _torch_libdir():
+    try:
+        import torch
+
+        return os.path.join(os.path.dirname(torch.__file__), "lib")
+    except Exception:  # pragma: no cover
+        return None
+
+
+def _needs_build(obj, src):
+    deps = [src, os.path.join(CSRC, "vj_common.h")]
+    return not os.path.exists(obj) or any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
+
+
+def build(verbose=True, force=False):
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    jobs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(objdir, s.replace(".hip", ".o"))
+        if force or _needs_build(obj, src):
+            jobs.append([HIPCC, *CFLAGS, "-c", src, "-o", obj])
+
+    def run(cmd):
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return cmd[-1]
+
+    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+        for o in ex.map(run, jobs):
+            if verbose:
+                print(f"[vjepa2_amd.build] compiled {os.path.basename(o)}", file=sys.stderr)
+    objs = [os.path.join(objdir, s.replace(".hip", ".o")) for s in SOURCES]
+    if force or jobs or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        tl = _torch_libdir()
+        if tl:
+            link += [f"-L{tl}", f"-Wl,-rpath,{tl}"]
+        run(link)
+        if verbose:
+            print(f"[vjepa2_amd.build] linked {LIB}", file=sys.stderr)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

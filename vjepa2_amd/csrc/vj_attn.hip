@@ -1,0 +1,548 @@
+// Varlen flash attention (non-causal, no dropout) for gfx950, forward + deterministic backward.
+// Replaces F.scaled_dot_product_attention in RoPEAttention.forward (src/models/utils/modules.py:367-372)
+// and Attention.forward (modules.py:411-418) for head_dim 64 (ViT encoders) and 32
+// (predictor, A9).
+//
+// Layout: tokens of all sequences are concatenated ("ragged batch"): q/k/v rows live in one
+// token-major bf16 buffer (the fused QKV GEMM output [T, 3*H*hd]), head h at column off + h*hd.
+// Sequences are described by up to 4 groups of equal-length sequences (both JEPA mask passes of a
+// step run as ONE launch). O is written token-major [T, H*hd] (= the proj GEMM's A operand).
+//
+// MFMA formulation (v_mfma_f32_32x32x16_bf16; accumulator: col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5)):
+//  forward, wave = 32 queries:  S^T = K Q^T (query on the lane -> softmax stats are per lane),
+//                               O^T += V^T P^T, P^T taken straight from the S^T accumulator (k-permuted),
+//                               V^T fragments by ds_read_b64_tr_b16.
+//  dK/dV kernel, wave = 32 keys: S = Q K^T, dP = dO V^T (key on the lane), dV^T += dO^T P, dK^T += Q^T dS.
+//  dQ kernel, wave = 32 queries: S^T = K Q^T, dP^T = V dO^T, dQ^T += K^T dS^T.
+// No atomics: dQ and dK/dV come from separate sweeps, so the backward is bitwise reproducible.
+// LDS images (one per tile, read both by rows and transposed): 16-B chunk index XOR-swizzled,
+//   HD=64 (128-B rows): sw(r) = (((r>>1)&1)<<2) | ((r>>2)&3);  HD=32 (64-B rows): sw(r) = (r>>2)&3.
+// Both keep ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads bank-conflict free.
+#include "vj_common.h"
+
+namespace {
+
+constexpr int MAXG = 4;
+struct SeqGroups {
+  int ngroups;
+  int nseq[MAXG];
+  int len[MAXG];
+  int tok0[MAXG];
+  int tiles_prefix[MAXG + 1];  // cumulative tile counts (tile size set by the kernel)
+};
+
+struct AttnArgs {
+  const bf16_t* qkv;  // q, k, v (RoPE already applied to q, k)
+  long ld;            // row stride of qkv (elements)
+  int q_off, k_off, v_off;
+  bf16_t* o;  // forward output / backward: dO input
+  long ldo;
+  const bf16_t* dout;  // backward: dO
+  long lddo;
+  float* stats;  // [2][H][T]: lse (natural log), delta = rowsum(dO*O)
+  bf16_t* dqkv;  // backward output, same layout as qkv
+  long ldd;
+  int H, T;
+  float scale;  // softmax scale (head_dim^-0.5)
+  SeqGroups sg;
+};
+
+// Locate (sequence start, length, tile index in sequence) of a flat tile id.
+__device__ __forceinline__ void locate(const SeqGroups& sg, int tile, int tiles_per_seq_div, int& seq_start,
+                                       int& len, int& t_in_seq) {
+  int g = 0;
+#pragma unroll
+  for (int i = 1; i < MAXG; ++i)
+    if (i < sg.ngroups && tile >= sg.tiles_prefix[i]) g = i;
+  const int local = tile - sg.tiles_prefix[g];
+  len = sg.len[g];
+  const int tps = (len + tiles_per_seq_div - 1) / tiles_per_seq_div;
+  const int s = local / tps;
+  t_in_seq = local - s * tps;
+  seq_start = sg.tok0[g] + s * len;
+}
+
+template <int HD>
+__device__ __forceinline__ int swz(int r) {
+  if constexpr (HD == 64) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+  else return (r >> 2) & 3;
+}
+template <int HD>
+__device__ __forceinline__ int lds_off(int r, int chunk) {  // byte offset of 16-B chunk
+  return r * (HD * 2) + ((chunk ^ swz<HD>(r)) * 16);
+}
+
+// Stage ROWS x HD bf16 rows starting at token row0 (< nvalid valid rows) into an LDS image.
+// Pieces of 1 KB (one wave-instruction); piece p handles rows [p*RPP, (p+1)*RPP).
+template <int HD, int ROWS>
+__device__ __forceinline__ void stage_rows(__amdgpu_buffer_rsrc_t rs, long ld, int row0, int nvalid,
+                                           LDS_AS char* lds, int wave, int lane, int nwaves) {
+  constexpr int CPR = HD / 8;          // 16-B chunks per row
+  constexpr int RPP = 64 / CPR;        // rows per piece
+  constexpr int PIECES = ROWS / RPP;
+  for (int p = wave; p < PIECES; p += nwaves) {
+    const int r = p * RPP + lane / CPR;
+    const int phys = lane % CPR;
+    const int c = phys ^ swz<HD>(r);
+    const bool ok = (row0 + r) < nvalid;
+    const uint32_t voff = ok ? (uint32_t)(((long)(row0 + r) * ld + c * 8) * 2) : VJ_OOB;
+    dma16(rs, lds + p * 1024, voff);
+  }
+}
+
+// A-operand row fragment (rows rb + lane&31, k-step s): 8 bf16 at chunk 2s + (lane>>5).
+template <int HD>
+__device__ __forceinline__ bf16x8 row_frag(const LDS_AS char* lds, int rb, int s, int lane) {
+  const int r = rb + (lane & 31);
+  return *(const LDS_AS bf16x8*)(lds + lds_off<HD>(r, 2 * s + (lane >> 5)));
+}
+// Transposed fragment: lane gets X[rows kb+8(j>>2)+4h+(j&3)][col cb + (lane&31)], j = 0..7
+// (the k-permuted order of an accumulator used as an operand).
+template <int HD>
+__device__ __forceinline__ bf16x8 tr_frag(const LDS_AS char* lds, int kb, int cb, int lane) {
+  const int h = lane >> 5;
+  const int q = (lane >> 2) & 3;
+  const int col = cb + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const int r0 = kb + 4 * h + q;
+  const int r1 = r0 + 8;
+  const int within = (col & 7) * 2;
+  const s16x4 lo = ds_read_tr16(lds + lds_off<HD>(r0, col >> 3) + within);
+  const s16x4 hi = ds_read_tr16(lds + lds_off<HD>(r1, col >> 3) + within);
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Accumulator registers 8s..8s+7 -> bf16 operand fragment.
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (__bf16)a[8 * s + j];
+  return v;
+}
+
+__device__ __forceinline__ bf16x8 gload8(const bf16_t* p, bool ok) {
+  if (!ok) {
+    bf16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+    return z;
+  }
+  return *(const bf16x8*)p;
+}
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+// ------------------------------------------------------------------------------------------------
+// Forward: block = 4 waves x 32 queries, KV tiles of 64 keys double-buffered in LDS.
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
+  constexpr int KT = 64;
+  constexpr int TB = KT * HD * 2;  // bytes per K or V tile
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
+  LDS_AS char* smem = (LDS_AS char*)smem_raw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = blockIdx.y;
+  int seq0, len, qt;
+  locate(a.sg, blockIdx.x, 128, seq0, len, qt);
+  const int qloc = qt * 128 + wave * 32 + (lane & 31);
+  const bool qok = qloc < len;
+  const int hl = lane >> 5;
+
+  // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[q][16s + 8h + j].
+  bf16x8 qf[HD / 16];
+  const bf16_t* qrow = a.qkv + (long)(seq0 + qloc) * a.ld + a.q_off + h * HD;
+#pragma unroll
+  for (int s = 0; s < HD / 16; ++s) qf[s] = gload8(qrow + 16 * s + 8 * hl, qok);
+
+  const bf16_t* kbase = a.qkv + (long)seq0 * a.ld + a.k_off + h * HD;
+  const bf16_t* vbase = a.qkv + (long)seq0 * a.ld + a.v_off + h * HD;
+  const uint32_t bytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
+  const __amdgpu_buffer_rsrc_t rk = make_rsrc(kbase, bytes);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(vbase, bytes);
+
+  f32x16 ot[HD / 32];
+#pragma unroll
+  for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ot[d][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+  const float c = a.scale * LOG2E;
+
+  const int nkt = (len + KT - 1) / KT;
+  stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
+  stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) {
+      LDS_AS char* nx = smem + (cur ^ 1) * 2 * TB;
+      stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
+      stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
+    }
+    const LDS_AS char* Ks = smem + cur * 2 * TB;
+    const LDS_AS char* Vs = Ks + TB;
+    f32x16 st[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < HD / 16; ++s)
+        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Ks, kk * 32, s, lane), qf[s], st[kk], 0, 0, 0);
+    }
+    // mask keys beyond the sequence; tile max
+    float mx = -INFINITY;
+    const int kb = kt * KT;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + kk * 32 + acc_row(r, lane);
+        if (key >= len) st[kk][r] = -INFINITY;
+        mx = fmaxf(mx, st[kk][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f((m_run - m_new) * c);
+    m_run = m_new;
+    float psum = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f((st[kk][r] - m_new) * c);
+        st[kk][r] = p;
+        psum += p;
+      }
+    l_run = l_run * alpha + psum;
+#pragma unroll
+    for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ot[d][r] *= alpha;
+    // O^T += V^T P^T over 4 key-steps of 16
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
+#pragma unroll
+      for (int d = 0; d < HD / 32; ++d)
+        ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<HD>(Vs, ks * 16, d * 32, lane), pf, ot[d], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = 1.f / l_tot;
+  if (qok) {
+    bf16_t* orow = a.o + (long)(seq0 + qloc) * a.ldo + h * HD;
+#pragma unroll
+    for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int col = d * 32 + acc_row(r, lane);
+        *(uint32_t*)(orow + col) = pack_bf2(ot[d][r] * inv, ot[d][r + 1] * inv);
+      }
+    if (hl == 0) a.stats[(long)h * a.T + seq0 + qloc] = m_run * a.scale + logf(l_tot);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// delta[h][t] = sum_d dO[t][h*hd+d] * O[t][h*hd+d]   (one thread per (token, head))
+template <int HD>
+__global__ void k_attn_delta(AttnArgs a) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)a.T * a.H) return;
+  const int t = (int)(i / a.H), h = (int)(i % a.H);
+  const bf16x8* o = (const bf16x8*)(a.o + (long)t * a.ldo + h * HD);
+  const bf16x8* g = (const bf16x8*)(a.dout + (long)t * a.lddo + h * HD);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < HD / 8; ++k) {
+    const bf16x8 x = o[k], y = g[k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += (float)x[j] * (float)y[j];
+  }
+  a.stats[(long)a.H * a.T + (long)h * a.T + t] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// dK/dV: block = 4 waves x 32 keys; sweep query tiles of 32 (Q, dO, lse, delta staged in LDS).
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
+  constexpr int QT = 32;
+  constexpr int TB = QT * HD * 2;
+  // per stage: Q tile, dO tile, 32 lse + 32 delta floats
+  constexpr int STAGE = 2 * TB + 256;
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  LDS_AS char* smem = (LDS_AS char*)smem_raw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = blockIdx.y;
+  int seq0, len, kt;
+  locate(a.sg, blockIdx.x, 128, seq0, len, kt);
+  const int kloc = kt * 128 + wave * 32 + (lane & 31);
+  const bool kok = kloc < len;
+  const int hl = lane >> 5;
+
+  // K^T and V^T fragments (B operands): lane holds K[key][16s + 8h + j].
+  bf16x8 kf[HD / 16], vf[HD / 16];
+  const bf16_t* krow = a.qkv + (long)(seq0 + kloc) * a.ld + a.k_off + h * HD;
+  const bf16_t* vrow = a.qkv + (long)(seq0 + kloc) * a.ld + a.v_off + h * HD;
+#pragma unroll
+  for (int s = 0; s < HD / 16; ++s) {
+    kf[s] = gload8(krow + 16 * s + 8 * hl, kok);
+    vf[s] = gload8(vrow + 16 * s + 8 * hl, kok);
+  }
+  const uint32_t qbytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
+  const uint32_t dbytes = (uint32_t)min((long)len * a.lddo * 2, 0x7fffffffL);
+  const __amdgpu_buffer_rsrc_t rq = make_rsrc(a.qkv + (long)seq0 * a.ld + a.q_off + h * HD, qbytes);
+  const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dout + (long)seq0 * a.lddo + h * HD, dbytes);
+  // stats: lse at [h][seq0 + i], delta at [H*T + h*T + seq0 + i]
+  const __amdgpu_buffer_rsrc_t rs =
+      make_rsrc(a.stats + (long)h * a.T + seq0, (uint32_t)min(((long)a.H * a.T + len) * 4, 0x7fffffffL));
+  const long dstat = (long)a.H * a.T;  // element distance lse -> delta
+
+  f32x16 dvt[HD / 32], dkt[HD / 32];
+#pragma unroll
+  for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dvt[d][r] = dkt[d][r] = 0.f;
+  const float c = a.scale * LOG2E;
+
+  auto stage = [&](int qt, LDS_AS char* st) {
+    stage_rows<HD, QT>(rq, a.ld, qt * QT, len, st, wave, lane, 4);
+    stage_rows<HD, QT>(rd, a.lddo, qt * QT, len, st + TB, wave, lane, 4);
+    if (wave == 3) {  // 64 lanes x 4 B: lanes 0-31 lse, 32-63 delta
+      const int i = qt * QT + (lane & 31);
+      const uint32_t voff = (i < len) ? (uint32_t)((i + (lane >= 32 ? dstat : 0)) * 4) : VJ_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, st + 2 * TB, 4, voff, 0, 0, 0);
+    }
+  };
+
+  const int nqt = (len + QT - 1) / QT;
+  stage(0, smem);
+  __syncthreads();
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int cur = qt & 1;
+    if (qt + 1 < nqt) stage(qt + 1, smem + (cur ^ 1) * STAGE);
+    const LDS_AS char* Qs = smem + cur * STAGE;
+    const LDS_AS char* Ds = Qs + TB;
+    const LDS_AS float* Ls = (const LDS_AS float*)(Qs + 2 * TB);
+    // S = Q K^T (rows: queries, col: key)
+    f32x16 sacc, dp;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sacc[r] = dp[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) {
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Qs, 0, s, lane), kf[s], sacc, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Ds, 0, s, lane), vf[s], dp, 0, 0, 0);
+    }
+    // P = exp(S*scale - lse); dS = P * (dP - delta)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = acc_row(r, lane);
+      const bool ok = kok && (qt * QT + qi < len);
+      const float lse = Ls[qi], dl = Ls[32 + qi];
+      const float p = ok ? exp2f(sacc[r] * c - lse * LOG2E) : 0.f;
+      sacc[r] = p;
+      dp[r] = p * (dp[r] - dl);
+    }
+    // dV^T += dO^T P ; dK^T += Q^T dS   (k-permuted accumulators as B operands)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pf = acc_frag(sacc, s2);
+      const bf16x8 sf = acc_frag(dp, s2);
+#pragma unroll
+      for (int d = 0; d < HD / 32; ++d) {
+        dvt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<HD>(Ds, s2 * 16, d * 32, lane), pf, dvt[d], 0, 0, 0);
+        dkt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<HD>(Qs, s2 * 16, d * 32, lane), sf, dkt[d], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  if (kok) {
+    bf16_t* dk = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.k_off + h * HD;
+    bf16_t* dv = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.v_off + h * HD;
+#pragma unroll
+    for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int col = d * 32 + acc_row(r, lane);
+        *(uint32_t*)(dk + col) = pack_bf2(dkt[d][r] * a.scale, dkt[d][r + 1] * a.scale);
+        *(uint32_t*)(dv + col) = pack_bf2(dvt[d][r], dvt[d][r + 1]);
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dQ: block = 4 waves x 32 queries; sweep key tiles of 64 (K, V staged in LDS).
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
+  constexpr int KT = 64;
+  constexpr int TB = KT * HD * 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
+  LDS_AS char* smem = (LDS_AS char*)smem_raw;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int h = blockIdx.y;
+  int seq0, len, qt;
+  locate(a.sg, blockIdx.x, 128, seq0, len, qt);
+  const int qloc = qt * 128 + wave * 32 + (lane & 31);
+  const bool qok = qloc < len;
+  const int hl = lane >> 5;
+
+  bf16x8 qf[HD / 16], gf[HD / 16];
+  const bf16_t* qrow = a.qkv + (long)(seq0 + qloc) * a.ld + a.q_off + h * HD;
+  const bf16_t* grow = a.dout + (long)(seq0 + qloc) * a.lddo + h * HD;
+#pragma unroll
+  for (int s = 0; s < HD / 16; ++s) {
+    qf[s] = gload8(qrow + 16 * s + 8 * hl, qok);
+    gf[s] = gload8(grow + 16 * s + 8 * hl, qok);
+  }
+  const float lse2 = qok ? a.stats[(long)h * a.T + seq0 + qloc] * LOG2E : 0.f;
+  const float dl = qok ? a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc] : 0.f;
+
+  const uint32_t bytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
+  const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.qkv + (long)seq0 * a.ld + a.k_off + h * HD, bytes);
+  const __amdgpu_buffer_rsrc_t rv = make_rsrc(a.qkv + (long)seq0 * a.ld + a.v_off + h * HD, bytes);
+
+  f32x16 dqt[HD / 32];
+#pragma unroll
+  for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dqt[d][r] = 0.f;
+  const float c = a.scale * LOG2E;
+
+  const int nkt = (len + KT - 1) / KT;
+  stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
+  stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) {
+      LDS_AS char* nx = smem + (cur ^ 1) * 2 * TB;
+      stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
+      stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
+    }
+    const LDS_AS char* Ks = smem + cur * 2 * TB;
+    const LDS_AS char* Vs = Ks + TB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      f32x16 st, dpt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[r] = dpt[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < HD / 16; ++s) {
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Ks, kk * 32, s, lane), qf[s], st, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Vs, kk * 32, s, lane), gf[s], dpt, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * KT + kk * 32 + acc_row(r, lane);
+        const bool ok = qok && key < len;
+        const float p = ok ? exp2f(st[r] * c - lse2) : 0.f;
+        dpt[r] = p * (dpt[r] - dl);
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bf16x8 sf = acc_frag(dpt, s2);
+#pragma unroll
+        for (int d = 0; d < HD / 32; ++d)
+          dqt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<HD>(Ks, kk * 32 + s2 * 16, d * 32, lane), sf,
+                                                           dqt[d], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  if (qok) {
+    bf16_t* dq = a.dqkv + (long)(seq0 + qloc) * a.ldd + a.q_off + h * HD;
+#pragma unroll
+    for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int col = d * 32 + acc_row(r, lane);
+        *(uint32_t*)(dq + col) = pack_bf2(dqt[d][r] * a.scale, dqt[d][r + 1] * a.scale);
+      }
+  }
+}
+
+int fill_groups(SeqGroups& sg, int ngroups, const int* nseq, const int* len, int tile, long T) {
+  VJ_CHECK_ARG(ngroups >= 1 && ngroups <= MAXG, "attention: 1..%d sequence groups supported (got %d)", MAXG, ngroups);
+  sg.ngroups = ngroups;
+  long tok = 0, tiles = 0;
+  for (int g = 0; g < MAXG; ++g) {
+    if (g < ngroups) {
+      VJ_CHECK_ARG(nseq[g] >= 0 && len[g] >= 1, "attention: bad group %d (nseq=%d len=%d)", g, nseq[g], len[g]);
+      sg.nseq[g] = nseq[g];
+      sg.len[g] = len[g];
+      sg.tok0[g] = (int)tok;
+      sg.tiles_prefix[g] = (int)tiles;
+      tok += (long)nseq[g] * len[g];
+      tiles += (long)nseq[g] * ((len[g] + tile - 1) / tile);
+    } else {
+      sg.nseq[g] = 0;
+      sg.len[g] = 1;
+      sg.tok0[g] = (int)tok;
+      sg.tiles_prefix[g] = (int)tiles;
+    }
+  }
+  sg.tiles_prefix[MAXG] = (int)tiles;
+  VJ_CHECK_ARG(tok == T, "attention: groups cover %ld tokens but T=%ld", tok, T);
+  return VJ_OK;
+}
+
+int check_common(int H, int hd, long ld, long ldo) {
+  VJ_CHECK_ARG(hd == 64 || hd == 32, "attention: head_dim must be 32 or 64 (got %d)", hd);
+  VJ_CHECK_ARG(H >= 1 && H <= 65535, "attention: bad H=%d", H);
+  VJ_CHECK_ARG(ld % 8 == 0 && ldo % 8 == 0, "attention: row strides must be multiples of 8");
+  return VJ_OK;
+}
+
+}  // namespace
+
+extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o,
+                           long ldo, float* lse_stats, float scale, int ngroups, const int* nseq, const int* len,
+                           void* stream) {
+  if (T == 0) return VJ_OK;
+  int rc = check_common(H, hd, ld, ldo);
+  if (rc) return rc;
+  AttnArgs a{};
+  a.qkv = (const bf16_t*)qkv; a.ld = ld; a.q_off = q_off; a.k_off = k_off; a.v_off = v_off;
+  a.o = (bf16_t*)o; a.ldo = ldo; a.stats = lse_stats; a.H = H; a.T = T; a.scale = scale;
+  rc = fill_groups(a.sg, ngroups, nseq, len, 128, T);
+  if (rc) return rc;
+  dim3 grid(a.sg.tiles_prefix[MAXG], H);
+  hipStream_t st = (hipStream_t)stream;
+  if (hd == 64) hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(k_attn_fwd<32>, grid, dim3(256), 0, st, a);
+  VJ_LAUNCH_CHECK("vj_attn_fwd");
+  return VJ_OK;
+}
+
+extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                           const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
+                           float scale, int ngroups, const int* nseq, const int* len, void* stream) {
+  if (T == 0) return VJ_OK;
+  int rc = check_common(H, hd, ld, ldo);
+  if (rc) return rc;
+  VJ_CHECK_ARG(lddo % 8 == 0 && ldd % 8 == 0, "vj_attn_bwd: strides must be multiples of 8");
+  AttnArgs a{};
+  a.qkv = (const bf16_t*)qkv; a.ld = ld; a.q_off = q_off; a.k_off = k_off; a.v_off = v_off;
+  a.o = (bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.stats = stats;
+  a.dqkv = (bf16_t*)dqkv; a.ldd = ldd; a.H = H; a.T = T; a.scale = scale;
+  rc = fill_groups(a.sg, ngroups, nseq, len, 128, T);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const long nth = (long)T * H;
+  const int dblocks = (int)((nth + 255) / 256);
+  dim3 grid(a.sg.tiles_prefix[MAXG], H);
+  if (hd == 64) {
+    hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_attn_bwd_dkdv<64>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_attn_bwd_dq<64>, grid, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_attn_bwd_dkdv<32>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_attn_bwd_dq<32>, grid, dim3(256), 0, st, a);
+  }
+  VJ_LAUNCH_CHECK("vj_attn_bwd");
+  return VJ_OK;
+}

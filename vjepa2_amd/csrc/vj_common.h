@@ -1,0 +1,89 @@
+// Shared helpers for the V-JEPA 2 gfx950 kernel library (libvjepa_hip.so).
+// CDNA4 only: wave64, MFMA bf16, LDS-DMA (buffer_load ... lds), ds_read_b64_tr_b16.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short bf16_t;  // storage type of a bf16 element in global memory
+
+#define LDS_AS __attribute__((address_space(3)))
+
+// ----- error reporting (C ABI: every entry point returns 0 or a VJ_ERR_* code) -----
+enum {
+  VJ_OK = 0,
+  VJ_ERR_ARG = 1,       // bad argument (shape / null pointer / alignment)
+  VJ_ERR_LAUNCH = 2,    // hipGetLastError after a launch
+  VJ_ERR_UNSUPPORTED = 3,
+};
+
+void vj_set_error(const char* fmt, ...);
+
+#define VJ_CHECK_ARG(cond, ...)          \
+  do {                                   \
+    if (!(cond)) {                       \
+      vj_set_error(__VA_ARGS__);         \
+      return VJ_ERR_ARG;                 \
+    }                                    \
+  } while (0)
+
+#define VJ_LAUNCH_CHECK(what)                                                    \
+  do {                                                                           \
+    hipError_t e_ = hipGetLastError();                                           \
+    if (e_ != hipSuccess) {                                                      \
+      vj_set_error("%s: launch failed: %s", what, hipGetErrorString(e_));        \
+      return VJ_ERR_LAUNCH;                                                      \
+    }                                                                            \
+  } while (0)
+
+// ----- bf16 <-> f32 (round-to-nearest-even; NaN-preserving via the hardware cvt) -----
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 on gfx950
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// ----- wave reductions (64 lanes) -----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ----- buffer resource (SRD) for LDS-DMA loads with hardware range check -----
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+// 16 bytes per lane, global(rsrc + voffset) -> LDS(lds_wave_base + lane*16). Out-of-range -> zeros.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, LDS_AS void* lds_wave_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_wave_base, 16, voff, 0, 0, 0);
+}
+#define VJ_OOB 0x80000000u
+
+__device__ __forceinline__ s16x4 ds_read_tr16(const LDS_AS void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)p);
+}
+
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+static inline int vj_cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,746 @@
+// Memory-bound kernels of the V-JEPA 2 train step (gfx950). All are HBM-bound: vectorised 16-B
+// accesses, one wave per row for row-wise ops, deterministic two-level reductions (no atomics).
+//
+//   LayerNorm fwd/bwd           nn.LayerNorm in Block (modules.py:556-563), encoder/predictor norm
+//   RoPE fwd/bwd (in place)     rotate_queries_or_keys (modules.py:26-50) on q,k of RoPEAttention (:343-365)
+//   tubelet im2col gather       PatchEmbed3D Conv3d (patch_embed.py:42-52) + apply_masks (masks/utils.py:9-21)
+//   row gather/scatter/fill/add apply_masks, predictor token assembly & (un)sort (predictor.py:182-242)
+//   stable-rank index build     torch.argsort(cat(masks_x, masks_y)) (predictor.py:210-217, 240)
+//   fused target-LN + L1 loss   forward_target F.layer_norm + loss_fn (app/vjepa/train.py:414-435)
+//   AdamW, finite-check, EMA    torch.optim.AdamW foreach math (app/vjepa/utils.py:239), train.py:456-465
+//   column sums (bias grads), f32->bf16 casts
+#include "vj_common.h"
+
+static_assert(sizeof(float4) == 16, "");
+
+namespace {
+
+// ------------------------------------------------------------------------------------------------
+// LayerNorm forward: wave per row. x f32 or bf16 [M, ldx]; y bf16 or f32 [M, ldy]; optional affine.
+constexpr int LN_MAXV = 8;  // float4 per lane -> D <= 64*4*8 = 2048
+
+template <bool XBF, bool YF32>
+__global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __restrict__ x, long ldx,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                float eps, void* __restrict__ y, long ldy, float* __restrict__ mean,
+                                                float* __restrict__ rstd) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float4 v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      if constexpr (XBF) {
+        const uint2 u = *(const uint2*)((const bf16_t*)x + row * ldx + c);
+        v[i] = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+      } else {
+        v[i] = *(const float4*)((const float*)x + row * ldx + c);
+      }
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+  }
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
+      q += a * a + b * b + cc * cc + d * d;
+    }
+  }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      float o[4] = {(v[i].x - mu) * rs, (v[i].y - mu) * rs, (v[i].z - mu) * rs, (v[i].w - mu) * rs};
+      if (gamma) {
+        const float4 g = *(const float4*)(gamma + c);
+        const float4 b = *(const float4*)(beta + c);
+        o[0] = o[0] * g.x + b.x; o[1] = o[1] * g.y + b.y; o[2] = o[2] * g.z + b.z; o[3] = o[3] * g.w + b.w;
+      }
+      if constexpr (YF32) {
+        *(float4*)((float*)y + row * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+        *(uint2*)((bf16_t*)y + row * ldy + c) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+      }
+    }
+  }
+  if (lane == 0) {
+    if (mean) mean[row] = mu;
+    if (rstd) rstd[row] = rs;
+  }
+}
+
+// LayerNorm backward. dy bf16 [M, lddy]; x f32 [M, ldx]; dres f32 [M, ldr] = (dres_in or 0) + dx;
+// optional bf16 copy of the resulting dres; per-block partials of dgamma/dbeta -> ws[blk][2][D].
+template <bool ACC>
+__global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __restrict__ dy, long lddy,
+                                                const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+                                                const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                const float* __restrict__ dres_in, long ldri, float* __restrict__ dres,
+                                                long ldr, bf16_t* __restrict__ dres_bf, long ldrb, float* __restrict__ ws) {
+  __shared__ float red[2][LN_MAXV * 256];  // D <= 2048
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float4 dg[LN_MAXV], db[LN_MAXV];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) dg[i] = db[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (long row = (long)blockIdx.x * 4 + wave; row < M; row += (long)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float4 xh[LN_MAXV], g[LN_MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      if (c < D) {
+        const float4 xv = *(const float4*)(x + row * ldx + c);
+        const uint2 u = *(const uint2*)(dy + row * lddy + c);
+        const float4 d = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+        xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+        db[i].x += d.x; db[i].y += d.y; db[i].z += d.z; db[i].w += d.w;
+        dg[i].x += d.x * xh[i].x; dg[i].y += d.y * xh[i].y; dg[i].z += d.z * xh[i].z; dg[i].w += d.w * xh[i].w;
+        float4 gm = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (gamma) gm = *(const float4*)(gamma + c);
+        g[i] = make_float4(d.x * gm.x, d.y * gm.y, d.z * gm.z, d.w * gm.w);
+        s1 += g[i].x + g[i].y + g[i].z + g[i].w;
+        s2 += g[i].x * xh[i].x + g[i].y * xh[i].y + g[i].z * xh[i].z + g[i].w * xh[i].w;
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      if (c < D) {
+        float4 dx = make_float4(rs * (g[i].x - m1 - xh[i].x * m2), rs * (g[i].y - m1 - xh[i].y * m2),
+                                rs * (g[i].z - m1 - xh[i].z * m2), rs * (g[i].w - m1 - xh[i].w * m2));
+        if constexpr (ACC) {
+          const float4 o = *(const float4*)(dres_in + row * ldri + c);
+          dx.x += o.x; dx.y += o.y; dx.z += o.z; dx.w += o.w;
+        }
+        *(float4*)(dres + row * ldr + c) = dx;
+        if (dres_bf)
+          *(uint2*)(dres_bf + row * ldrb + c) = make_uint2(pack_bf2(dx.x, dx.y), pack_bf2(dx.z, dx.w));
+      }
+    }
+  }
+  if (!ws) return;
+  // block reduction of the per-wave dgamma/dbeta partials, waves added in fixed order (deterministic)
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int i = 0; i < LN_MAXV; ++i) {
+        const int c = (i * 64 + lane) * 4;
+        if (c < D) {
+          float4* a = (float4*)&red[0][c];
+          float4* b = (float4*)&red[1][c];
+          if (w == 0) {
+            *a = dg[i];
+            *b = db[i];
+          } else {
+            const float4 x = *a, y = *b;
+            *a = make_float4(x.x + dg[i].x, x.y + dg[i].y, x.z + dg[i].z, x.w + dg[i].w);
+            *b = make_float4(y.x + db[i].x, y.y + db[i].y, y.z + db[i].z, y.w + db[i].w);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int c = threadIdx.x; c < D; c += 256) {
+    ws[(long)blockIdx.x * 2 * D + c] = red[0][c];
+    ws[(long)blockIdx.x * 2 * D + D + c] = red[1][c];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Column sums. Stage 1: ws[s][n] = sum over rows in slice s. Stage 2: out[n] (+)= sum_s ws[s][n].
+template <bool BF>
+__global__ void k_colsum1(int M, int N, const void* __restrict__ x, long ld, int rows_per_slice, float* __restrict__ ws) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const long r0 = (long)blockIdx.y * rows_per_slice;
+  const long r1 = min((long)M, r0 + rows_per_slice);
+  float s = 0.f;
+  for (long r = r0; r < r1; ++r) {
+    if constexpr (BF) s += bf2f(((const bf16_t*)x)[r * ld + n]);
+    else s += ((const float*)x)[r * ld + n];
+  }
+  ws[(long)blockIdx.y * N + n] = s;
+}
+__global__ void k_colsum2(int S, int N, const float* __restrict__ ws, long ws_ld, float* __restrict__ out, int acc) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int i = 0; i < S; ++i) s += ws[(long)i * ws_ld + n];
+  out[n] = acc ? out[n] + s : s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// RoPE on q and k of a [T, ld] bf16 qkv buffer, in place. Per head: three rotated slices of width
+// sw = 2*((hd/3)/2) (depth, height, width positions), rest untouched. Element j of a slice uses
+// angle theta_{j mod sw/2}; partner y_{2i} = -x_{2i+1}, y_{2i+1} = x_{2i} (modules.py:43-50).
+// Angles come from host-built tables cos/sin[pos][i] (computed with the reference's fp32 ops).
+// Thread = one 8-element chunk of one head of q or k.
+__global__ void k_rope(int T, int H, int hd, bf16_t* __restrict__ qkv, long ld, int q_off, int k_off,
+                       const int* __restrict__ ids, int ids_mod, int tpf, int tpr, const float* __restrict__ ctab,
+                       const float* __restrict__ stab, int half, int inverse) {
+  const int cpr = hd / 8;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)T * 2 * H * cpr;
+  if (i >= total) return;
+  const int chunk = (int)(i % cpr);
+  long rest = i / cpr;
+  const int h = (int)(rest % H);
+  rest /= H;
+  const int which = (int)(rest % 2);
+  const long t = rest / 2;
+  const int sw = 2 * half;
+  const int e0 = chunk * 8;
+  if (e0 >= 3 * sw) return;  // untouched tail
+  const int id = ids ? ids[t] : (int)(t % ids_mod);
+  const int fr = id / tpf;
+  const int hr = (id - tpf * fr) / tpr;
+  const int wc = (id - tpf * fr) - tpr * hr;
+  bf16_t* p = qkv + t * ld + (which ? k_off : q_off) + h * hd + e0;
+  uint4 u = *(uint4*)p;
+  bf16_t v[8];
+  *(uint4*)v = u;
+  float x[8], o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = bf2f(v[j]);
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const int e = e0 + j;  // even element index within the head
+    if (e >= 3 * sw) {
+      o[j] = x[j];
+      o[j + 1] = x[j + 1];
+      continue;
+    }
+    const int ax = e / sw;
+    const int js = e - ax * sw;  // even position within the slice
+    const int pos = ax == 0 ? fr : (ax == 1 ? hr : wc);
+    const int f0 = js % half, f1 = (js + 1) % half;
+    const float c0 = ctab[pos * half + f0], s0 = stab[pos * half + f0];
+    const float c1 = ctab[pos * half + f1], s1 = stab[pos * half + f1];
+    if (!inverse) {
+      o[j] = x[j] * c0 - x[j + 1] * s0;
+      o[j + 1] = x[j + 1] * c1 + x[j] * s1;
+    } else {  // transpose of the forward map (gradient)
+      o[j] = x[j] * c0 + x[j + 1] * s1;
+      o[j + 1] = -x[j] * s0 + x[j + 1] * c1;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = f2bf(o[j]);
+  *(uint4*)p = *(uint4*)v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Tubelet im2col (Conv3d k = s = (tub, p, p) as a GEMM operand), gathering only the listed tokens.
+// clip f32 [B, C, Tf, Hf, Wf]; row r -> (b, token) with token = idx ? idx[r] : r % N, b = r / K.
+// out bf16 [R, C*tub*p*p], column = c*tub*p*p + kt*p*p + kh*p + kw (= Conv3d weight flattening).
+__global__ void k_im2col(int R, int K, const long* __restrict__ idx, int C, int Tf, int Hf, int Wf, int tub,
+                         int pch, const float* __restrict__ clip, bf16_t* __restrict__ out) {
+  const int r = blockIdx.x;
+  if (r >= R) return;
+  const int b = r / K;
+  const int Hp = Hf / pch, Wp = Wf / pch;
+  const int tok = idx ? (int)idx[r] : (r % K);
+  const int tt = tok / (Hp * Wp), hh = (tok % (Hp * Wp)) / Wp, ww = tok % Wp;
+  const int kdim = C * tub * pch * pch;
+  // each thread handles 4 consecutive kw of one (c, kt, kh) row: pch % 4 == 0
+  const int nq = kdim / 4;
+  for (int q = threadIdx.x; q < nq; q += blockDim.x) {
+    const int col = q * 4;
+    const int kw = col % pch;
+    const int kh = (col / pch) % pch;
+    const int kt = (col / (pch * pch)) % tub;
+    const int c = col / (pch * pch * tub);
+    const float* src = clip + ((((long)b * C + c) * Tf + (tt * tub + kt)) * Hf + (hh * pch + kh)) * Wf + ww * pch + kw;
+    const float4 v = *(const float4*)src;
+    *(uint2*)(out + (long)r * kdim + col) = make_uint2(pack_bf2(v.x, v.y), pack_bf2(v.z, v.w));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Row ops (bit-exact copies). elem = 2 or 4 bytes; ncols*elem % 16 == 0 handled by 4-B lanes.
+__global__ void k_gather_rows(int R, int rowbytes, const char* __restrict__ src, long lds, const int* __restrict__ idx,
+                              char* __restrict__ dst, long ldd, int scatter) {
+  const int r = blockIdx.x;
+  if (r >= R) return;
+  const long sr = scatter ? r : idx[r];
+  const long dr = scatter ? idx[r] : r;
+  const uint4* s = (const uint4*)(src + sr * lds);
+  uint4* d = (uint4*)(dst + dr * ldd);
+  for (int i = threadIdx.x; i < rowbytes / 16; i += blockDim.x) d[i] = s[i];
+}
+
+// dst[idx[r]] = vec (f32 row broadcast; mask tokens)
+__global__ void k_fill_rows(int R, int D, float* __restrict__ dst, long ldd, const int* __restrict__ idx,
+                            const float* __restrict__ vec) {
+  const int r = blockIdx.x;
+  if (r >= R) return;
+  float* d = dst + (long)idx[r] * ldd;
+  for (int i = threadIdx.x; i < D; i += blockDim.x) d[i] = vec[i];
+}
+
+// dst[r] += table[idx[r]]   (sincos positional embeddings, non-RoPE variant)
+__global__ void k_add_rows(int R, int D, float* __restrict__ dst, long ldd, const float* __restrict__ table,
+                           long ldt, const int* __restrict__ idx, int idx_mod) {
+  const int r = blockIdx.x;
+  if (r >= R) return;
+  const long t = idx ? idx[r] : (r % idx_mod);
+  for (int i = threadIdx.x; i < D; i += blockDim.x) dst[(long)r * ldd + i] += table[t * ldt + i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Predictor index build for one (masks_x, masks_y) pair (predictor.py:206-242): per row b, the
+// stable rank of every element of cat(mx[b], my[b]) (= torch.argsort for unique ids), written as
+//   pos[row0 + b*n + rank]      = id          (RoPE positions of the sorted sequence)
+//   ctx_dst[b*K + i]            = row0 + b*n + rank(i)        (where context token i goes)
+//   tgt_rows[b*Kp + j]          = row0 + b*n + rank(K + j)    (where target token j sits)
+//   loss_rows[b*Kp + j]         = (b % bmod)*N + my[b][j]     (row of the target-encoder output)
+// One block per b; ids staged in LDS; O(n^2) compares (n <= ~8k).
+__global__ void k_pred_index(int K, int Kp, const long* __restrict__ mx, const long* __restrict__ my, int row0,
+                             int bmod, int N, int* __restrict__ pos, int* __restrict__ ctx_dst,
+                             int* __restrict__ tgt_rows, int* __restrict__ loss_rows) {
+  extern __shared__ int ids[];
+  const int b = blockIdx.x;
+  const int n = K + Kp;
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    ids[i] = (int)(i < K ? mx[(long)b * K + i] : my[(long)b * Kp + (i - K)]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int v = ids[i];
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+      const int w = ids[j];
+      rank += (w < v) || (w == v && j < i);
+    }
+    const int dst = row0 + b * n + rank;
+    pos[dst] = v;
+    if (i < K) ctx_dst[(long)b * K + i] = dst;
+    else {
+      tgt_rows[(long)b * Kp + (i - K)] = dst;
+      if (loss_rows) loss_rows[(long)b * Kp + (i - K)] = (b % bmod) * N + v;
+    }
+  }
+}
+
+// int64 mask [B, K] -> int32 token ids (RoPE positions of a context pass)
+__global__ void k_ids64to32(long n, const long* __restrict__ in, int* __restrict__ out) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int)in[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused target normalisation + JEPA L1 loss (+ gradient), wave per predicted row:
+//   h   = LN2(LN1(tgt[loss_rows[r]]; gamma, beta, eps1); eps2)     (encoder norm, then F.layer_norm)
+//   d   = z[r] - h;  row_loss[r] = w_g * sum |d|^p / p;  dz[r] = w_g * |d|^(p-1) * sign(d)
+// with w_g = 1 / (rows_g * D * ngroups) for the mask group g of row r (train.py:425-435).
+struct LossGroups {
+  int ngroups;
+  int rows[4];
+};
+__global__ __launch_bounds__(256) void k_jepa_loss(int R, int D, const float* __restrict__ z, long ldz,
+                                                   const float* __restrict__ tgt, long ldt,
+                                                   const int* __restrict__ loss_rows, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, float eps1, float eps2, float p,
+                                                   LossGroups lg, bf16_t* __restrict__ dz, long lddz,
+                                                   float* __restrict__ row_loss) {
+  const int lane = threadIdx.x & 63;
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  int g = 0;
+  long acc = lg.rows[0];
+  while (g < lg.ngroups - 1 && r >= acc) acc += lg.rows[++g];
+  const float w = 1.f / ((float)lg.rows[g] * (float)D * (float)lg.ngroups);
+  const float* t = tgt + (long)loss_rows[r] * ldt;
+  float4 v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      v[i] = *(const float4*)(t + c);
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+  }
+  float mu = wave_sum(s) / D, q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
+      q += a * a + b * b + cc * cc + d * d;
+    }
+  }
+  float rs = rsqrtf(wave_sum(q) / D + eps1);
+  s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      const float4 gm = *(const float4*)(gamma + c);
+      const float4 bt = *(const float4*)(beta + c);
+      v[i] = make_float4((v[i].x - mu) * rs * gm.x + bt.x, (v[i].y - mu) * rs * gm.y + bt.y,
+                         (v[i].z - mu) * rs * gm.z + bt.z, (v[i].w - mu) * rs * gm.w + bt.w);
+      s += v[i].x + v[i].y + v[i].z + v[i].w;
+    }
+  }
+  mu = wave_sum(s) / D;
+  q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
+      q += a * a + b * b + cc * cc + d * d;
+    }
+  }
+  rs = rsqrtf(wave_sum(q) / D + eps2);
+  float lsum = 0.f;
+  const bool p1 = (p == 1.f);
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < D) {
+      const float4 zv = *(const float4*)(z + r * ldz + c);
+      const float hv[4] = {(v[i].x - mu) * rs, (v[i].y - mu) * rs, (v[i].z - mu) * rs, (v[i].w - mu) * rs};
+      const float zz[4] = {zv.x, zv.y, zv.z, zv.w};
+      float gd[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = zz[j] - hv[j];
+        const float ad = fabsf(d);
+        const float sg = (d > 0.f) ? 1.f : ((d < 0.f) ? -1.f : 0.f);
+        if (p1) {
+          lsum += ad;
+          gd[j] = w * sg;
+        } else {
+          lsum += powf(ad, p) / p;
+          gd[j] = w * powf(ad, p - 1.f) * sg;
+        }
+      }
+      *(uint2*)(dz + r * lddz + c) = make_uint2(pack_bf2(gd[0], gd[1]), pack_bf2(gd[2], gd[3]));
+    }
+  }
+  lsum = wave_sum(lsum);
+  if (lane == 0) row_loss[r] = lsum * w;
+}
+
+// Deterministic final reduction: out[0] = sum_i in[i] (one block, fixed order).
+__global__ void k_sum1(long n, const float* __restrict__ in, float* __restrict__ out) {
+  __shared__ float red[256];
+  float s = 0.f;
+  for (long i = threadIdx.x; i < n; i += 256) s += in[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Optimizer / EMA over flat fp32 arenas (float4 per thread; n % 4 == 0).
+__global__ void k_check_finite(long n4, const float4* __restrict__ g, int* __restrict__ found_inf) {
+  bool bad = false;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = g[i];
+    bad |= !isfinite(v.x) || !isfinite(v.y) || !isfinite(v.z) || !isfinite(v.w);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) *found_inf = 1;
+}
+
+struct AdamHP {
+  float decay;       // 1 - lr * weight_decay
+  float beta1, beta2;
+  float one_m_b1, one_m_b2;
+  float neg_step;    // -(lr / (1 - beta1^t))
+  float bc2_sqrt;    // sqrt(1 - beta2^t)
+  float eps;
+  float grad_scale;  // gradients are multiplied by this first (1/world for an unaveraged sum)
+};
+__global__ void k_adamw(long n4, float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ m,
+                        float4* __restrict__ v, uint2* __restrict__ pbf, AdamHP hp, const int* __restrict__ found_inf) {
+  if (found_inf && *found_inf) return;  // GradScaler.step semantics: skip the update on inf/NaN
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float pp[4], gg[4], mm[4], vv[4];
+    *(float4*)pp = p[i];
+    *(float4*)gg = g[i];
+    *(float4*)mm = m[i];
+    *(float4*)vv = v[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gr = gg[j] * hp.grad_scale;
+      pp[j] = pp[j] * hp.decay;
+      mm[j] = mm[j] + hp.one_m_b1 * (gr - mm[j]);
+      vv[j] = vv[j] * hp.beta2;
+      vv[j] = vv[j] + hp.one_m_b2 * gr * gr;
+      const float den = sqrtf(vv[j]) / hp.bc2_sqrt + hp.eps;
+      pp[j] = pp[j] + hp.neg_step * (mm[j] / den);
+    }
+    p[i] = *(float4*)pp;
+    m[i] = *(float4*)mm;
+    v[i] = *(float4*)vv;
+    if (pbf) pbf[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+  }
+}
+
+// target <- target * m + (1 - m) * online   (two roundings, as _foreach_mul_ + _foreach_add_)
+__global__ void k_ema(long n4, float4* __restrict__ t, const float4* __restrict__ e, float mom, float one_m,
+                      uint2* __restrict__ tbf) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    float a[4], b[4];
+    *(float4*)a = t[i];
+    *(float4*)b = e[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = a[j] * mom;
+      a[j] = x + one_m * b[j];
+    }
+    t[i] = *(float4*)a;
+    if (tbf) tbf[i] = make_uint2(pack_bf2(a[0], a[1]), pack_bf2(a[2], a[3]));
+  }
+}
+
+__global__ void k_cast_bf16(long n4, const float4* __restrict__ in, uint2* __restrict__ out) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = in[i];
+    out[i] = make_uint2(pack_bf2(v.x, v.y), pack_bf2(v.z, v.w));
+  }
+}
+
+inline int grid_stride_blocks(long n4) {
+  long b = (n4 + 255) / 256;
+  return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
+}
+
+}  // namespace
+
+// ================================================================================================
+// C ABI
+extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma,
+                                const float* beta, float eps, void* y, int y_f32, long ldy, float* mean, float* rstd,
+                                void* stream) {
+  if (M == 0) return VJ_OK;
+  VJ_CHECK_ARG(D % 4 == 0 && D <= 64 * 4 * LN_MAXV, "vj_layernorm_fwd: D=%d must be %%4 and <= 2048", D);
+  VJ_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "vj_layernorm_fwd: gamma/beta both or neither");
+  VJ_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "vj_layernorm_fwd: strides must be %%4");
+  dim3 grid((M + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+  if (x_bf16 && y_f32) hipLaunchKernelGGL((k_ln_fwd<true, true>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
+  else if (x_bf16) hipLaunchKernelGGL((k_ln_fwd<true, false>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
+  else if (y_f32) hipLaunchKernelGGL((k_ln_fwd<false, true>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
+  else hipLaunchKernelGGL((k_ln_fwd<false, false>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
+  VJ_LAUNCH_CHECK("vj_layernorm_fwd");
+  return VJ_OK;
+}
+
+extern "C" int vj_layernorm_bwd_blocks(int M) {
+  const int b = (M + 3) / 4;
+  return b < 512 ? (b > 0 ? b : 1) : 512;
+}
+
+extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate,
+                             float* ws, long ws_floats, void* stream);
+
+extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const float* x, long ldx, const float* mean,
+                                const float* rstd, const float* gamma, const float* dres_in, long ldri, float* dres,
+                                long ldr, void* dres_bf16, long ldrb, float* dgamma, float* dbeta, float* ws,
+                                long ws_floats, void* stream) {
+  if (M == 0) return VJ_OK;
+  VJ_CHECK_ARG(D % 4 == 0 && D <= 64 * 4 * LN_MAXV, "vj_layernorm_bwd: bad D=%d", D);
+  const int nb = vj_layernorm_bwd_blocks(M);
+  const bool want_g = dgamma || dbeta;
+  if (want_g) {
+    VJ_CHECK_ARG(ws && ws_floats >= (long)nb * 2 * D, "vj_layernorm_bwd: workspace needs %ld floats", (long)nb * 2 * D);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  float* part = want_g ? ws : nullptr;
+  if (dres_in)
+    hipLaunchKernelGGL(k_ln_bwd<true>, dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd,
+                       gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part);
+  else
+    hipLaunchKernelGGL(k_ln_bwd<false>, dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd,
+                       gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part);
+  VJ_LAUNCH_CHECK("vj_layernorm_bwd");
+  if (want_g) {
+    // partials laid out [nb][2][D]: dgamma column sums over rows of stride 2D
+    if (dgamma) hipLaunchKernelGGL(k_colsum2, dim3((D + 255) / 256), dim3(256), 0, st, nb, D, ws, 2L * D, dgamma, 1);
+    if (dbeta) hipLaunchKernelGGL(k_colsum2, dim3((D + 255) / 256), dim3(256), 0, st, nb, D, ws + D, 2L * D, dbeta, 1);
+    VJ_LAUNCH_CHECK("vj_layernorm_bwd(reduce)");
+  }
+  return VJ_OK;
+}
+
+extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate, float* ws,
+                             long ws_floats, void* stream) {
+  if (N == 0) return VJ_OK;
+  int S = (M + 255) / 256;
+  if (S > 128) S = 128;
+  if (S < 1) S = 1;
+  VJ_CHECK_ARG(ws && ws_floats >= (long)S * N, "vj_colsum_f32: workspace needs %ld floats", (long)S * N);
+  const int rps = (M + S - 1) / S;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g1((N + 255) / 256, S);
+  if (x_bf16) hipLaunchKernelGGL(k_colsum1<true>, g1, dim3(256), 0, st, M, N, x, ld, rps, ws);
+  else hipLaunchKernelGGL(k_colsum1<false>, g1, dim3(256), 0, st, M, N, x, ld, rps, ws);
+  hipLaunchKernelGGL(k_colsum2, dim3((N + 255) / 256), dim3(256), 0, st, S, N, ws, (long)N, out, accumulate);
+  VJ_LAUNCH_CHECK("vj_colsum_f32");
+  return VJ_OK;
+}
+
+extern "C" int vj_rope(int T, int H, int hd, void* qkv, long ld, int q_off, int k_off, const int* ids, int ids_mod,
+                       int tokens_per_frame, int tokens_per_row, const float* cos_tab, const float* sin_tab, int half,
+                       int inverse, void* stream) {
+  if (T == 0) return VJ_OK;
+  VJ_CHECK_ARG(hd % 8 == 0 && ld % 8 == 0 && q_off % 8 == 0 && k_off % 8 == 0, "vj_rope: alignment");
+  VJ_CHECK_ARG(half == (hd / 3) / 2 && half >= 1, "vj_rope: half=%d inconsistent with hd=%d", half, hd);
+  VJ_CHECK_ARG(ids || ids_mod > 0, "vj_rope: ids or ids_mod required");
+  const long total = (long)T * 2 * H * (hd / 8);
+  hipLaunchKernelGGL(k_rope, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, T, H, hd,
+                     (bf16_t*)qkv, ld, q_off, k_off, ids, ids_mod, tokens_per_frame, tokens_per_row, cos_tab, sin_tab,
+                     half, inverse);
+  VJ_LAUNCH_CHECK("vj_rope");
+  return VJ_OK;
+}
+
+extern "C" int vj_im2col_tubelet(int R, int K, const long* idx, int B, int C, int Tf, int Hf, int Wf, int tub, int pch,
+                                 const float* clip, void* out, void* stream) {
+  if (R == 0) return VJ_OK;
+  VJ_CHECK_ARG(pch % 4 == 0 && Tf % tub == 0 && Hf % pch == 0 && Wf % pch == 0, "vj_im2col_tubelet: bad geometry");
+  VJ_CHECK_ARG(R <= (long)B * K, "vj_im2col_tubelet: R=%d > B*K", R);
+  hipLaunchKernelGGL(k_im2col, dim3(R), dim3(256), 0, (hipStream_t)stream, R, K, idx, C, Tf, Hf, Wf, tub, pch, clip,
+                     (bf16_t*)out);
+  VJ_LAUNCH_CHECK("vj_im2col_tubelet");
+  return VJ_OK;
+}
+
+extern "C" int vj_gather_rows(int R, int rowbytes, const void* src, long src_ld_bytes, const int* idx, void* dst,
+                              long dst_ld_bytes, int scatter, void* stream) {
+  if (R == 0) return VJ_OK;
+  VJ_CHECK_ARG(rowbytes % 16 == 0 && src_ld_bytes % 16 == 0 && dst_ld_bytes % 16 == 0, "vj_gather_rows: 16-B rows");
+  hipLaunchKernelGGL(k_gather_rows, dim3(R), dim3(64), 0, (hipStream_t)stream, R, rowbytes, (const char*)src,
+                     src_ld_bytes, idx, (char*)dst, dst_ld_bytes, scatter);
+  VJ_LAUNCH_CHECK("vj_gather_rows");
+  return VJ_OK;
+}
+
+extern "C" int vj_fill_rows(int R, int D, float* dst, long ldd, const int* idx, const float* vec, void* stream) {
+  if (R == 0) return VJ_OK;
+  hipLaunchKernelGGL(k_fill_rows, dim3(R), dim3(128), 0, (hipStream_t)stream, R, D, dst, ldd, idx, vec);
+  VJ_LAUNCH_CHECK("vj_fill_rows");
+  return VJ_OK;
+}
+
+extern "C" int vj_add_rows(int R, int D, float* dst, long ldd, const float* table, long ldt, const int* idx,
+                           int idx_mod, void* stream) {
+  if (R == 0) return VJ_OK;
+  VJ_CHECK_ARG(idx || idx_mod > 0, "vj_add_rows: idx or idx_mod");
+  hipLaunchKernelGGL(k_add_rows, dim3(R), dim3(128), 0, (hipStream_t)stream, R, D, dst, ldd, table, ldt, idx, idx_mod);
+  VJ_LAUNCH_CHECK("vj_add_rows");
+  return VJ_OK;
+}
+
+extern "C" int vj_pred_index(int B, int K, int Kp, const long* mx, const long* my, int row0, int bmod, int N, int* pos,
+                             int* ctx_dst, int* tgt_rows, int* loss_rows, void* stream) {
+  if (B == 0) return VJ_OK;
+  const int n = K + Kp;
+  VJ_CHECK_ARG(n >= 1 && n <= 16384, "vj_pred_index: sequence length %d out of range", n);
+  hipLaunchKernelGGL(k_pred_index, dim3(B), dim3(256), n * sizeof(int), (hipStream_t)stream, K, Kp, mx, my, row0,
+                     bmod > 0 ? bmod : B, N, pos, ctx_dst, tgt_rows, loss_rows);
+  VJ_LAUNCH_CHECK("vj_pred_index");
+  return VJ_OK;
+}
+
+extern "C" int vj_ids64to32(long n, const long* in, int* out, void* stream) {
+  if (n == 0) return VJ_OK;
+  hipLaunchKernelGGL(k_ids64to32, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, in, out);
+  VJ_LAUNCH_CHECK("vj_ids64to32");
+  return VJ_OK;
+}
+
+extern "C" int vj_jepa_loss(int R, int D, const float* z, long ldz, const float* tgt, long ldt, const int* loss_rows,
+                            const float* gamma, const float* beta, float eps1, float eps2, float loss_exp,
+                            int ngroups, const int* group_rows, void* dz, long lddz, float* row_loss, float* loss_out,
+                            void* stream) {
+  if (R == 0) return VJ_OK;
+  VJ_CHECK_ARG(D % 4 == 0 && D <= 2048, "vj_jepa_loss: bad D=%d", D);
+  VJ_CHECK_ARG(ngroups >= 1 && ngroups <= 4, "vj_jepa_loss: 1..4 groups");
+  LossGroups lg{};
+  lg.ngroups = ngroups;
+  long tot = 0;
+  for (int i = 0; i < ngroups; ++i) {
+    lg.rows[i] = group_rows[i];
+    tot += group_rows[i];
+  }
+  VJ_CHECK_ARG(tot == R, "vj_jepa_loss: groups cover %ld rows, R=%d", tot, R);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_jepa_loss, dim3((R + 3) / 4), dim3(256), 0, st, R, D, z, ldz, tgt, ldt, loss_rows, gamma, beta,
+                     eps1, eps2, loss_exp, lg, (bf16_t*)dz, lddz, row_loss);
+  hipLaunchKernelGGL(k_sum1, dim3(1), dim3(256), 0, st, (long)R, row_loss, loss_out);
+  VJ_LAUNCH_CHECK("vj_jepa_loss");
+  return VJ_OK;
+}
+
+extern "C" int vj_check_finite(long n, const float* g, int* found_inf, void* stream) {
+  if (n == 0) return VJ_OK;
+  VJ_CHECK_ARG(n % 4 == 0 && ((uintptr_t)g & 15) == 0, "vj_check_finite: n %% 4 and 16-B alignment");
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(k_check_finite, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4,
+                     (const float4*)g, found_inf);
+  VJ_LAUNCH_CHECK("vj_check_finite");
+  return VJ_OK;
+}
+
+extern "C" int vj_adamw(long n, float* p, const float* g, float* m, float* v, void* p_bf16, float lr, float beta1,
+                        float beta2, float eps, float weight_decay, int step, float grad_scale, const int* found_inf,
+                        void* stream) {
+  if (n == 0) return VJ_OK;
+  VJ_CHECK_ARG(n % 4 == 0, "vj_adamw: n must be %%4");
+  VJ_CHECK_ARG(step >= 1, "vj_adamw: step must be >= 1");
+  AdamHP hp;
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  hp.decay = (float)(1.0 - (double)lr * (double)weight_decay);
+  hp.beta1 = beta1;
+  hp.beta2 = beta2;
+  hp.one_m_b1 = (float)(1.0 - (double)beta1);
+  hp.one_m_b2 = (float)(1.0 - (double)beta2);
+  hp.neg_step = (float)(-((double)lr / bc1));
+  hp.bc2_sqrt = (float)sqrt(bc2);
+  hp.eps = eps;
+  hp.grad_scale = grad_scale;
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(k_adamw, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4, (float4*)p,
+                     (const float4*)g, (float4*)m, (float4*)v, (uint2*)p_bf16, hp, found_inf);
+  VJ_LAUNCH_CHECK("vj_adamw");
+  return VJ_OK;
+}
+
+extern "C" int vj_ema(long n, float* target, const float* online, float momentum, void* target_bf16, void* stream) {
+  if (n == 0) return VJ_OK;
+  VJ_CHECK_ARG(n % 4 == 0, "vj_ema: n must be %%4");
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(k_ema, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4, (float4*)target,
+                     (const float4*)online, momentum, (float)(1.0 - (double)momentum), (uint2*)target_bf16);
+  VJ_LAUNCH_CHECK("vj_ema");
+  return VJ_OK;
+}
+
+extern "C" int vj_cast_bf16(long n, const float* in, void* out, void* stream) {
+  if (n == 0) return VJ_OK;
+  VJ_CHECK_ARG(n % 4 == 0, "vj_cast_bf16: n must be %%4");
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(k_cast_bf16, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4,
+                     (const float4*)in, (uint2*)out);
+  VJ_LAUNCH_CHECK("vj_cast_bf16");
+  return VJ_OK;
+}

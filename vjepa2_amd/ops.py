@@ -1,0 +1,276 @@
+"""Tensor-level wrappers over the HIP kernels (libvjepa_hip.so).
+
+Every function validates shapes/dtypes/devices on the host (so a kernel never sees an operand it
+was not written for), then enqueues the kernel on torch's current HIP stream. No CPU fallback.
+"""
+
+import torch
+
+from ._lib import call, int_array
+
+EPI_BF16, EPI_F32, EPI_F32_RESID, EPI_GELU, EPI_GELU_BWD = 0, 1, 2, 3, 4
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("vjepa2_amd ops require device (HIP) tensors; there is no CPU path")
+
+
+def _rowmajor(t, name):
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a 2-D row-major tensor (stride(1)==1), got {tuple(t.shape)} {t.stride()}")
+    return t.stride(0)
+
+
+# ------------------------------------------------------------------------------------------------
+# GEMMs (nn.Linear forward / dgrad / wgrad)
+def gemm(M, N, K, a, lda, a_kmajor, b, ldb, b_kmajor, epi, out=None, ldc=0, out2=None, ldc2=0, bias=None, aux=None,
+         ldaux=0):
+    _dev(a, b, out, out2, bias, aux)
+    if a.dtype != BF16 or b.dtype != BF16:
+        raise TypeError("gemm operands must be bf16")
+    if bias is not None and (bias.dtype != F32 or bias.numel() < N):
+        raise TypeError("gemm bias must be f32 [N]")
+    call("vj_gemm_bf16", M, N, K, _p(a), lda, int(a_kmajor), _p(b), ldb, int(b_kmajor), epi, _p(bias), _p(aux), ldaux,
+         _p(out), ldc, _p(out2), ldc2, _stream())
+
+
+def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
+    """Y = X W^T + b.  x bf16 [M,K] row-major, w bf16 [N,K].  Returns the output tensor(s)."""
+    M, K = x.shape
+    N = w.shape[0]
+    assert w.shape[1] == K, (tuple(x.shape), tuple(w.shape))
+    lda = _rowmajor(x, "x")
+    ldb = _rowmajor(w, "w")
+    if epi == EPI_BF16:
+        out = out if out is not None else torch.empty(M, N, dtype=BF16, device=x.device)
+    elif epi in (EPI_F32, EPI_F32_RESID):
+        out = out if out is not None else torch.empty(M, N, dtype=F32, device=x.device)
+        if epi == EPI_F32_RESID:
+            assert resid is not None and resid.dtype == F32 and resid.shape == (M, N)
+    elif epi == EPI_GELU:
+        out2 = out2 if out2 is not None else torch.empty(M, N, dtype=BF16, device=x.device)
+    ldc = out.stride(0) if out is not None else 0
+    ldc2 = out2.stride(0) if out2 is not None else 0
+    gemm(M, N, K, x, lda, True, w, ldb, True, epi, out=out, ldc=ldc, out2=out2, ldc2=ldc2, bias=bias,
+         aux=resid, ldaux=resid.stride(0) if resid is not None else 0)
+    return (out, out2) if epi == EPI_GELU else out
+
+
+def linear_dgrad(dy, w, out=None, gelu_pre=None):
+    """dX = dY W (bf16 out); with gelu_pre: dX = (dY W) * GELU'(pre)."""
+    M, N = dy.shape
+    K = w.shape[1]
+    assert w.shape[0] == N
+    out = out if out is not None else torch.empty(M, K, dtype=BF16, device=dy.device)
+    epi = EPI_GELU_BWD if gelu_pre is not None else EPI_BF16
+    gemm(M, K, N, dy, _rowmajor(dy, "dy"), True, w, _rowmajor(w, "w"), False, epi, out=out, ldc=out.stride(0),
+         aux=gelu_pre, ldaux=gelu_pre.stride(0) if gelu_pre is not None else 0)
+    return out
+
+
+def linear_wgrad(dy, x, dw):
+    """dW[N,K] += dY^T X  (f32 accumulate into dw)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    assert x.shape[0] == M and dw.shape == (N, K) and dw.dtype == F32
+    gemm(N, K, M, dy, _rowmajor(dy, "dy"), False, x, _rowmajor(x, "x"), False, EPI_F32_RESID, out=dw,
+         ldc=dw.stride(0), aux=dw, ldaux=dw.stride(0))
+    return dw
+
+
+# ------------------------------------------------------------------------------------------------
+def colsum(x, out, accumulate=True):
+    """out[n] (+)= sum_m x[m, n]; x bf16 or f32 [M,N]."""
+    _dev(x, out)
+    M, N = x.shape
+    S = min(128, max(1, (M + 255) // 256))
+    ws = torch.empty(S * N, dtype=F32, device=x.device)
+    call("vj_colsum_f32", M, N, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(out), int(accumulate), _p(ws),
+         ws.numel(), _stream())
+    return out
+
+
+def layernorm_fwd(x, weight, bias, eps, out_dtype=BF16, want_stats=True):
+    _dev(x)
+    M, D = x.shape
+    y = torch.empty(M, D, dtype=out_dtype, device=x.device)
+    mean = torch.empty(M, dtype=F32, device=x.device) if want_stats else None
+    rstd = torch.empty(M, dtype=F32, device=x.device) if want_stats else None
+    call("vj_layernorm_fwd", M, D, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(weight), _p(bias), float(eps),
+         _p(y), int(out_dtype == F32), D, _p(mean), _p(rstd), _stream())
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, weight, dres_in=None, dweight=None, dbias=None, want_bf16=False):
+    """Returns (dres f32 = dres_in + dLN/dx, optional bf16 copy). Accumulates dweight/dbias."""
+    _dev(dy, x)
+    M, D = x.shape
+    assert dy.dtype == BF16 and dy.shape == (M, D)
+    dres = torch.empty(M, D, dtype=F32, device=x.device)
+    dres_bf = torch.empty(M, D, dtype=BF16, device=x.device) if want_bf16 else None
+    ws = None
+    nws = 0
+    if dweight is not None or dbias is not None:
+        from ._lib import load
+
+        nb = load().vj_layernorm_bwd_blocks(M)
+        nws = nb * 2 * D
+        ws = torch.empty(nws, dtype=F32, device=x.device)
+    call("vj_layernorm_bwd", M, D, _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x"), _p(mean), _p(rstd),
+         _p(weight), _p(dres_in), dres_in.stride(0) if dres_in is not None else 0, _p(dres), D, _p(dres_bf), D,
+         _p(dweight), _p(dbias), _p(ws), nws, _stream())
+    return dres, dres_bf
+
+
+def rope_(qkv, H, hd, q_off, k_off, ids, ids_mod, tpf, tpr, cos_tab, sin_tab, inverse=False):
+    _dev(qkv, ids, cos_tab, sin_tab)
+    T = qkv.shape[0]
+    if ids is not None:
+        assert ids.dtype == torch.int32 and ids.numel() == T
+    half = (hd // 3) // 2
+    call("vj_rope", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, _p(ids), int(ids_mod), int(tpf), int(tpr),
+         _p(cos_tab), _p(sin_tab), half, int(inverse), _stream())
+
+
+def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None):
+    """groups: list of (nseq, len). Returns (O bf16 [T, H*hd], stats f32 [2, H, T])."""
+    _dev(qkv)
+    T = qkv.shape[0]
+    D = H * hd
+    q_off = 0 if q_off is None else q_off
+    k_off = D if k_off is None else k_off
+    v_off = 2 * D if v_off is None else v_off
+    o = torch.empty(T, D, dtype=BF16, device=qkv.device)
+    stats = torch.empty(2, H, T, dtype=F32, device=qkv.device)
+    ns, ln = [g[0] for g in groups], [g[1] for g in groups]
+    call("vj_attn_fwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, v_off, _p(o), D, _p(stats),
+         float(scale), len(groups), int_array(ns), int_array(ln), _stream())
+    return o, stats
+
+
+def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None):
+    _dev(qkv, o, do, stats)
+    T = qkv.shape[0]
+    D = H * hd
+    dqkv = dqkv if dqkv is not None else torch.empty(T, 3 * D, dtype=BF16, device=qkv.device)
+    ns, ln = [g[0] for g in groups], [g[1] for g in groups]
+    call("vj_attn_bwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
+         _rowmajor(do, "do"), _p(stats), _p(dqkv), _rowmajor(dqkv, "dqkv"), float(scale), len(groups), int_array(ns),
+         int_array(ln), _stream())
+    return dqkv
+
+
+def im2col(clip, patch, tub, idx=None, K=None):
+    """clip f32 [B,C,T,H,W] -> bf16 [R, C*tub*p*p]; idx int64 [B,K] kept tokens (or all tokens)."""
+    _dev(clip, idx)
+    assert clip.dtype == F32 and clip.is_contiguous()
+    B, C, Tf, Hf, Wf = clip.shape
+    N = (Tf // tub) * (Hf // patch) * (Wf // patch)
+    if idx is not None:
+        assert idx.dtype == torch.int64 and idx.is_contiguous() and idx.shape[0] == B
+        K = idx.shape[1]
+    else:
+        K = N
+    R = B * K
+    out = torch.empty(R, C * tub * patch * patch, dtype=BF16, device=clip.device)
+    call("vj_im2col_tubelet", R, K, _p(idx), B, C, Tf, Hf, Wf, tub, patch, _p(clip), _p(out), _stream())
+    return out
+
+
+def gather_rows(src, idx, out=None, nrows=None):
+    """out[r] = src[idx[r]] (bit-exact)."""
+    _dev(src, idx)
+    R = idx.numel()
+    out = out if out is not None else torch.empty(R, src.shape[1], dtype=src.dtype, device=src.device)
+    es = src.element_size()
+    call("vj_gather_rows", R, src.shape[1] * es, _p(src), _rowmajor(src, "src") * es, _p(idx), _p(out),
+         _rowmajor(out, "out") * es, 0, _stream())
+    return out
+
+
+def scatter_rows(src, idx, out):
+    """out[idx[r]] = src[r] (bit-exact)."""
+    _dev(src, idx, out)
+    R = idx.numel()
+    es = src.element_size()
+    call("vj_gather_rows", R, src.shape[1] * es, _p(src), _rowmajor(src, "src") * es, _p(idx), _p(out),
+         _rowmajor(out, "out") * es, 1, _stream())
+    return out
+
+
+def fill_rows(dst, idx, vec):
+    _dev(dst, idx, vec)
+    call("vj_fill_rows", idx.numel(), dst.shape[1], _p(dst), _rowmajor(dst, "dst"), _p(idx), _p(vec), _stream())
+
+
+def add_rows(dst, table, idx=None, idx_mod=0):
+    _dev(dst, table, idx)
+    call("vj_add_rows", dst.shape[0], dst.shape[1], _p(dst), _rowmajor(dst, "dst"), _p(table),
+         _rowmajor(table, "table"), _p(idx), int(idx_mod), _stream())
+
+
+def pred_index(mx, my, row0, N, pos, ctx_dst, tgt_rows, loss_rows=None):
+    _dev(mx, my)
+    B, K = mx.shape
+    Kp = my.shape[1]
+    assert mx.dtype == torch.int64 and my.dtype == torch.int64 and mx.is_contiguous() and my.is_contiguous()
+    call("vj_pred_index", B, K, Kp, _p(mx), _p(my), int(row0), B, int(N), _p(pos), _p(ctx_dst), _p(tgt_rows),
+         _p(loss_rows), _stream())
+
+
+def ids64to32(x, out=None):
+    _dev(x)
+    assert x.dtype == torch.int64 and x.is_contiguous()
+    out = out if out is not None else torch.empty(x.numel(), dtype=torch.int32, device=x.device)
+    call("vj_ids64to32", x.numel(), _p(x), _p(out), _stream())
+    return out
+
+
+def jepa_loss(z, tgt, loss_rows, gamma, beta, group_rows, eps1=1e-6, eps2=1e-5, loss_exp=1.0):
+    """Returns (loss f32 [1], dz bf16 like z, row_loss f32 [R]). z f32 [R, D]."""
+    _dev(z, tgt, loss_rows)
+    assert z.dtype == F32, "jepa_loss: z must be f32"
+    R, D = z.shape
+    dz = torch.empty(R, D, dtype=BF16, device=z.device)
+    row_loss = torch.empty(R, dtype=F32, device=z.device)
+    loss = torch.empty(1, dtype=F32, device=z.device)
+    call("vj_jepa_loss", R, D, _p(z), _rowmajor(z, "z"), _p(tgt), _rowmajor(tgt, "tgt"), _p(loss_rows), _p(gamma),
+         _p(beta), float(eps1), float(eps2), float(loss_exp), len(group_rows), int_array(group_rows), _p(dz), D,
+         _p(row_loss), _p(loss), _stream())
+    return loss, dz, row_loss
+
+
+def check_finite(g, found_inf):
+    _dev(g, found_inf)
+    call("vj_check_finite", g.numel(), _p(g), _p(found_inf), _stream())
+
+
+def adamw(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, found_inf=None):
+    _dev(p, g, m, v, p_bf16, found_inf)
+    call("vj_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), float(lr), float(beta1), float(beta2),
+         float(eps), float(weight_decay), int(step), float(grad_scale), _p(found_inf), _stream())
+
+
+def ema(target, online, momentum, target_bf16=None):
+    _dev(target, online, target_bf16)
+    call("vj_ema", target.numel(), _p(target), _p(online), float(momentum), _p(target_bf16), _stream())
+
+
+def cast_bf16(x, out=None):
+    _dev(x)
+    assert x.dtype == F32 and x.is_contiguous()
+    out = out if out is not None else torch.empty(x.shape, dtype=BF16, device=x.device)
+    call("vj_cast_bf16", x.numel(), _p(x), _p(out), _stream())
+    return out

@@ -1,0 +1,218 @@
+"""Benchmark: V-JEPA 2 ViT-L/16 16x256^2 JEPA train step (fwd + bwd + AdamW + EMA), bf16, synthetic.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   (one rank per GPU)
+
+Workload (BASELINE.json configs[1]; per-GPU batch 24 = configs/train/vitl16/pretrain-256px-16f.yaml):
+ViT-L/16 RoPE encoder (24x1024, 16 heads), EMA target encoder, predictor 12x384 (12 heads), the two
+reference mask configs (8 blocks @15 %, 2 blocks @70 %), masks from the reference MaskCollator
+(torch seed 239 + rank), synthetic randn clips already resident in HBM. Weak scaling: every rank
+runs B=24 clips per step; RCCL all-reduce of the 326 M fp32 gradients per step for N > 1.
+
+Output: ONE JSON line (rank 0). `roofline` is the dominant kernel (largest total time) measured with
+HIP events around each of its launches inside the timed region; `cpu_baseline` times the CPU
+oracle (oracle/vjepa_oracle.py, fp32) on a bounded sample of the same workload.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "clips/sec/GPU (ViT-L/16, 16×256², bf16) fwd+bwd; 1→8 GPU scaling"
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+MASK_CFGS = [
+    dict(aspect_ratio=[0.75, 1.5], full_complement=False, max_keep=None, max_temporal_keep=1.0, num_blocks=8,
+         spatial_scale=[0.15, 0.15], temporal_scale=[1.0, 1.0]),
+    dict(aspect_ratio=[0.75, 1.5], full_complement=False, max_keep=None, max_temporal_keep=1.0, num_blocks=2,
+         spatial_scale=[0.7, 0.7], temporal_scale=[1.0, 1.0]),
+]
+MODELS = {"vit_large": dict(D=1024, depth=24, heads=16, mlp=4096), "vit_small": dict(D=384, depth=12, heads=6, mlp=1536),
+          "vit_giant_xformers": dict(D=1408, depth=40, heads=22, mlp=6144)}
+
+
+def step_flops(model, B, N, masks_enc, masks_pred, pd=384, pdepth=12, pmlp=1536, kdim=1536):
+    """SURVEY §8d algorithmic FLOPs of one step (no recompute, bwd = 2x fwd)."""
+    cfg = MODELS[model]
+    D, depth, mlp = cfg["D"], cfg["depth"], cfg["mlp"]
+
+    def lin(n, d, h):
+        return 2 * n * (4 * d * d + 2 * d * h)
+
+    def att(n, d):
+        return 4 * n * n * d
+
+    f = B * (depth * (lin(N, D, mlp) + att(N, D)) + 2 * N * kdim * D)
+    for me, mp in zip(masks_enc, masks_pred):
+        K, Kp = me.shape[1], mp.shape[1]
+        n = K + Kp
+        f += B * 3 * (depth * (lin(K, D, mlp) + att(K, D)) + 2 * K * kdim * D * 2 / 3)
+        f += B * 3 * (pdepth * (lin(n, pd, pmlp) + att(n, pd)) + 2 * K * D * pd + 2 * Kp * pd * D)
+    return f
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=24)
+    ap.add_argument("--model", default="vit_large")
+    ap.add_argument("--crop", type=int, default=256)
+    ap.add_argument("--frames", type=int, default=16)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--kernel-events", type=int, default=1)
+    args = ap.parse_args()
+
+    from vjepa2_amd import ops
+    from vjepa2_amd.distributed import init_distributed
+    from vjepa2_amd.masks import MaskCollator
+    from vjepa2_amd.train import JEPATrainer, init_opt, init_video_model
+    import torch.distributed as dist
+
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local_rank)
+    world, rank = init_distributed()
+    dev = torch.device("cuda", local_rank)
+    B, T, S = args.batch, args.frames, args.crop
+    N = (T // 2) * (S // 16) ** 2
+
+    torch.manual_seed(239)
+    enc, pred = init_video_model(device=dev, patch_size=16, max_num_frames=T, tubelet_size=2, model_name=args.model,
+                                 crop_size=S, pred_depth=12, pred_num_heads=12, pred_embed_dim=384, uniform_power=True,
+                                 use_mask_tokens=True, num_mask_tokens=6, zero_init_mask_tokens=True, use_sdpa=True,
+                                 use_rope=True)
+    import copy
+
+    tgt = copy.deepcopy(enc)
+    opt, scaler, sched, wds = init_opt(enc, pred, iterations_per_epoch=300, start_lr=1e-4, ref_lr=5.25e-4, warmup=40,
+                                       num_epochs=10, wd=0.04, final_wd=0.04, final_lr=5.25e-4, ipe_scale=1.25,
+                                       mixed_precision=True)
+    trainer = JEPATrainer(enc, pred, tgt, opt, mixed_precision=True, loss_exp=1.0, world_size=world)
+
+    # inputs resident in HBM before timing: clips + masks for every step (dataloader prefetch)
+    torch.manual_seed(239 + rank)
+    mc = MaskCollator(cfgs_mask=MASK_CFGS, dataset_fpcs=[T], crop_size=S, patch_size=16, tubelet_size=2)
+    nsteps = args.warmup + args.steps
+    data = []
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    nclip = min(nsteps, 4)
+    clips = [torch.randn(B, 3, T, S, S, device=dev, generator=g) for _ in range(nclip)]
+    for i in range(nsteps):
+        (_, me, mp), = mc([(torch.zeros(1), 0, [torch.arange(T)]) for _ in range(B)])
+        data.append((clips[i % nclip], [m.to(dev) for m in me], [m.to(dev) for m in mp]))
+    torch.cuda.synchronize()
+
+    def run(i):
+        c, me, mp = data[i]
+        sched.step()
+        wds.step()
+        return trainer.train_step([c], [me], [mp], 0.99925)
+
+    for i in range(args.warmup):
+        run(i)
+    torch.cuda.synchronize()
+
+    prof = ops.KernelEvents() if args.kernel_events else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    if prof:
+        prof.start()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, nsteps):
+        loss = run(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if prof:
+        prof.stop()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms = elapsed * 1000.0 / args.steps
+    total_clips = B * world * args.steps
+    value = total_clips / elapsed
+    flops = sum(step_flops(args.model, B, N, d[1], d[2]) for d in data[args.warmup:]) / args.steps
+
+    roof = None
+    kstats = None
+    if prof:
+        kstats = prof.summary()
+        dom = max(kstats, key=lambda k: kstats[k]["total_ms"])
+        st = kstats[dom]
+        achieved = st["flops"] / (st["total_ms"] * 1e-3) / 1e12
+        roof = {"kernel": dom, "bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                "launches_per_step": st["count"] / args.steps, "avg_launch_us": round(st["total_ms"] * 1e3 / st["count"], 2),
+                "flops_per_launch": st["flops"] / st["count"]}
+
+    cpu = None
+    if rank == 0 and args.cpu_baseline:
+        cpu = cpu_baseline(args, data[0])
+
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+               "config": {"workload": f"{args.model} (RoPE) + predictor 12x384, {T}x{S}^2 clips, B={B}/GPU, JEPA "
+                                      "train step: target fwd + ctx fwd/bwd (2 masks) + predictor fwd/bwd + L1 + "
+                                      "AdamW + EMA", "model": args.model, "global_batch": B * world,
+                          "seq_len": N, "parallelism": f"dp{world}"},
+               "clips_per_s_per_gpu": round(value / world, 3), "step_tflop": round(flops / 1e12, 2),
+               "step_tflops_per_gpu": round(flops / (ms * 1e-3) / 1e12, 1),
+               "mfu_bf16": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+               "loss_last": round(float(loss.item()), 5), "roofline": roof, "cpu_baseline": cpu}
+        if kstats:
+            out["kernels"] = {k: {"ms_per_step": round(v["total_ms"] / args.steps, 3), "count_per_step": v["count"] / args.steps,
+                                  "tflops": round(v["flops"] / (v["total_ms"] * 1e-3) / 1e12, 1) if v["flops"] else None}
+                              for k, v in sorted(kstats.items(), key=lambda kv: -kv[1]["total_ms"])}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, sample):
+    """The CPU oracle (fp32, the reference algorithm restated) on a bounded sample: ONE clip of the same
+    workload (ViT-L 16x256^2, the same two masks truncated to B=1), one full step. ~10-30 s."""
+    from oracle import vjepa_oracle as orc
+
+    threads = int(os.environ.get("VJ_CPU_THREADS", "16"))
+    torch.set_num_threads(threads)
+    torch.manual_seed(239)
+    from vjepa2_amd import vision_transformer as vt
+    from vjepa2_amd.predictor import vit_predictor
+
+    T, S = args.frames, args.crop
+    enc = getattr(vt, args.model)(img_size=S, num_frames=T, tubelet_size=2, use_rope=True, uniform_power=True)
+    pred = vit_predictor(img_size=S, use_mask_tokens=True, patch_size=16, num_frames=T, tubelet_size=2,
+                         embed_dim=enc.embed_dim, predictor_embed_dim=384, depth=12, num_heads=12, uniform_power=True,
+                         num_mask_tokens=6, use_rope=True)
+    ecfg = dict(patch_size=16, tubelet_size=2, num_heads=enc.num_heads, depth=len(enc.blocks), use_rope=True)
+    pcfg = dict(num_heads=12, depth=12, use_rope=True, grid_size=S // 16, num_mask_tokens=6,
+                num_patches=(T // 2) * (S // 16) ** 2)
+    tr = orc.OracleTrainer(enc.state_dict(), pred.state_dict(), ecfg, pcfg)
+    clips = sample[0][:1].cpu()
+    me = [m[:1].cpu() for m in sample[1]]
+    mp = [m[:1].cpu() for m in sample[2]]
+    t0 = time.perf_counter()
+    tr.step(clips, me, mp, 5.25e-4, 0.04, 0.99925)
+    dt = time.perf_counter() - t0
+    return {"value": round(1.0 / dt, 4), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"1 clip ({args.model} {T}x{S}^2, masks K={[m.shape[1] for m in me]}, "
+                      f"Kp={[m.shape[1] for m in mp]}), one full fp32 step (fwd+bwd+AdamW+EMA) of the CPU oracle, "
+                      f"{dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

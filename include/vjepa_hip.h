@@ -43,6 +43,12 @@ enum {
 int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb, int b_kmajor,
                  int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc, void* C2, long ldc2,
                  void* stream);
+/* Same with deterministic split-K over K (weight gradients: K = tokens, small M x N): blockIdx.z
+ * computes a K slice into ws [splitk][M][N] (f32), then one pass sums the slices in fixed order and
+ * applies the epilogue (BF16 / F32 / F32_RESID only). ws >= splitk*M*N floats. */
+int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                        int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
+                        void* C2, long ldc2, int splitk, float* ws, long ws_floats, void* stream);
 
 /* Varlen non-causal flash attention, head_dim 32 or 64 (F.scaled_dot_product_attention,
  * modules.py:367-372 / 411-418). Tokens of `ngroups` groups of equal-length sequences are
@@ -68,7 +74,7 @@ int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const float* x, lo
                      const float* rstd, const float* gamma, const float* dres_in, long ldri, float* dres, long ldr,
                      void* dres_bf16, long ldrb, float* dgamma, float* dbeta, float* ws, long ws_floats, void* stream);
 
-/* out[n] (+)= sum_m x[m, n]  (bias gradients). ws >= min(128, ceil(M/256)) * N floats. */
+/* out[n] (+)= sum_m x[m, n]  (bias gradients), N % 8 == 0. ws >= min(256, ceil(M/64)) * N floats. */
 int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate, float* ws,
                   long ws_floats, void* stream);
 
@@ -103,9 +109,12 @@ int vj_pred_index(int B, int K, int Kp, const long* mx, const long* my, int row0
 int vj_ids64to32(long n, const long* in, int* out, void* stream);
 
 /* Fused forward_target normalisation + JEPA loss + dL/dz (train.py:414-435). */
-int vj_jepa_loss(int R, int D, const float* z, long ldz, const float* tgt, long ldt, const int* loss_rows,
+/* z: predictor output rows (bf16 if z_bf16 else f32); rows split into ngroups mask groups of
+ * group_rows[g] rows; per-row weight pair_weight / (group_rows[g] * D). dz is bf16. */
+int vj_jepa_loss(int R, int D, const void* z, int z_bf16, long ldz, const float* tgt, long ldt, const int* loss_rows,
                  const float* gamma, const float* beta, float eps1, float eps2, float loss_exp, int ngroups,
-                 const int* group_rows, void* dz, long lddz, float* row_loss, float* loss_out, void* stream);
+                 const int* group_rows, float pair_weight, void* dz, long lddz, float* row_loss, float* loss_out,
+                 void* stream);
 
 /* Optimizer and EMA over flat fp32 arenas (torch.optim.AdamW foreach math, app/vjepa/utils.py:239;
  * GradScaler inf-skip train.py:446-451; EMA train.py:456-465). p_bf16 / target_bf16: optional

@@ -257,3 +257,44 @@ def adamw_step(p, g, m, v, step, lr, wd, beta1=0.9, beta2=0.999, eps=1e-8):
 def ema_update(target, online, m):
     target.mul_(m)
     target.add_(online, alpha=1 - m)
+
+
+# ------------------------------------------------------------------------------------------------
+class OracleTrainer:
+    """app/vjepa/train.py:409-471 restated on CPU fp32: per-mask encoder/predictor calls
+    (wrappers.py:20-43), L1 loss, autograd backward, AdamW over the 4 param groups of
+    app/vjepa/utils.py:224-237 (params with no gradient are skipped, as torch.optim does), EMA."""
+
+    def __init__(self, enc_sd, pred_sd, enc_cfg, pred_cfg, betas=(0.9, 0.999), eps=1e-8, loss_exp=1.0):
+        self.enc = {k: v.detach().clone().float().requires_grad_(k != "pos_embed") for k, v in enc_sd.items()}
+        self.pred = {k: v.detach().clone().float().requires_grad_(k != "predictor_pos_embed")
+                     for k, v in pred_sd.items()}
+        self.tgt = {k: v.detach().clone().float() for k, v in enc_sd.items()}
+        self.enc_cfg, self.pred_cfg = enc_cfg, pred_cfg
+        self.betas, self.eps, self.loss_exp = betas, eps, loss_exp
+        self.state = {}
+
+    def loss(self, clips, masks_enc, masks_pred):
+        with torch.no_grad():
+            h = forward_target(clips, self.tgt, self.enc_cfg)
+        z = [encoder_forward(clips, self.enc, self.enc_cfg, masks=m) for m in masks_enc]
+        z = [predictor_forward(zi, mx, my, self.pred, self.pred_cfg, mask_index=0)
+             for zi, mx, my in zip(z, masks_enc, masks_pred)]
+        return jepa_loss(z, h, masks_pred, self.loss_exp)
+
+    def step(self, clips, masks_enc, masks_pred, lr, wd, momentum):
+        loss = self.loss(clips, masks_enc, masks_pred)
+        loss.backward()
+        with torch.no_grad():
+            for sd in (self.enc, self.pred):
+                for k, p in sd.items():
+                    if not p.requires_grad or p.grad is None:
+                        continue
+                    st = self.state.setdefault(id(p), dict(m=torch.zeros_like(p), v=torch.zeros_like(p), t=0))
+                    st["t"] += 1
+                    decay = 0.0 if ("bias" in k or p.dim() == 1) else wd
+                    adamw_step(p, p.grad, st["m"], st["v"], st["t"], lr, decay, *self.betas, self.eps)
+                    p.grad = None
+            for k in self.tgt:
+                ema_update(self.tgt[k], self.enc[k].detach(), momentum)
+        return loss.item()

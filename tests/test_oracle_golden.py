@@ -1,0 +1,115 @@
+"""CPU: pin the oracle (oracle/vjepa_oracle.py) to the REFERENCE's own outputs (tests/golden/*.pt,
+produced by tests/golden/make_golden.py running weipeilun/vjepa2 on CPU, fp32)."""
+
+import os
+
+import pytest
+import torch
+
+from oracle import vjepa_oracle as orc
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gold(name):
+    return torch.load(os.path.join(GOLD, name), weights_only=True)
+
+
+def close(a, b, tol, what):
+    err = (a.detach().float() - b.detach().float()).abs().max().item()
+    scale = b.detach().float().abs().max().item() + 1e-12
+    assert err <= tol * max(1.0, scale), f"{what}: max err {err:.3e} (scale {scale:.3e})"
+
+
+def test_rope_golden():
+    g = gold("rope.pt")
+    for s in (20, 10):
+        close(orc.rotate_queries_or_keys(g[f"x{s}"], g[f"pos{s}"]), g[f"out{s}"], 1e-6, f"rope{s}")
+    close(orc.rotate_queries_or_keys(g["x_flat"], g["pos_flat"]), g["out_flat"], 1e-6, "rope flat")
+
+
+def test_sincos_golden():
+    g = gold("sincos.pt")
+    for up in (0, 1):
+        t = torch.from_numpy(orc.sincos_3d(96, 4, 2, uniform_power=bool(up)))
+        assert torch.equal(t, g[f"f64_up{up}"])
+
+
+def test_product_sincos_table_matches_reference():
+    from vjepa2_amd.vision_transformer import sincos_3d_table
+
+    g = gold("sincos.pt")
+    for up in (0, 1):
+        assert torch.equal(torch.from_numpy(sincos_3d_table(96, 4, 2, bool(up))), g[f"f64_up{up}"])
+
+
+@pytest.mark.parametrize("fixture", ["block_enc.pt", "block_pred.pt"])
+def test_block_golden(fixture):
+    g = gold(fixture)
+    c = g["cfg"]
+    sd = {k: v.clone().requires_grad_(True) for k, v in g["state"].items()}
+    x = g["x"].clone().requires_grad_(True)
+    grid = c["grid"]
+    tpf, tpr = grid * grid, grid  # with T/H/W given the same square grid results
+    y = orc.block(x, sd, "", c["heads"], ids=g["mask"], tokens_per_frame=tpf, tokens_per_row=tpr)
+    close(y, g["y"], 1e-5, "block y")
+    y.backward(g["gy"])
+    close(x.grad, g["gx"], 1e-5, "block dx")
+    for n, v in g["gparams"].items():
+        close(sd[n].grad, v, 1e-5, f"block d{n}")
+
+
+@pytest.mark.parametrize("rope", [1, 0])
+def test_encoder_golden(rope):
+    g = gold(f"encoder_rope{rope}.pt")
+    sd = {k: v.clone().requires_grad_(k != "pos_embed") for k, v in g["state"].items()}
+    cfg = dict(patch_size=16, tubelet_size=2, num_heads=1, depth=2, use_rope=bool(rope))
+    close(orc.encoder_forward(g["x"], sd, cfg), g["full"], 1e-5, "encoder full")
+    outs = [orc.encoder_forward(g["x"], sd, cfg, masks=m) for m in g["masks"]]
+    for o, e in zip(outs, g["outs"]):
+        close(o, e, 1e-5, "encoder masked")
+    sum((o * gy).sum() for o, gy in zip(outs, g["gys"])).backward()
+    for n, v in g["gparams"].items():
+        close(sd[n].grad, v, 1e-5, f"encoder d{n}")
+
+
+def test_predictor_golden():
+    g = gold("predictor.pt")
+    sd = {k: v.clone().requires_grad_(k != "predictor_pos_embed") for k, v in g["state"].items()}
+    cfg = dict(num_heads=3, depth=2, use_rope=True, grid_size=2, num_mask_tokens=2, num_patches=8)
+    for inp, exp, gy in zip(g["ins"], g["outs"], g["gys"]):
+        z = inp["z"].clone().requires_grad_(True)
+        o = orc.predictor_forward(z, inp["mx"], inp["my"], sd, cfg, mask_index=inp["mask_index"])
+        close(o, exp, 1e-5, "predictor out")
+        (o * gy).sum().backward()
+        close(z.grad, inp["gz"], 1e-5, "predictor dz")
+    for n, v in g["gparams"].items():
+        close(sd[n].grad, v, 1e-5, f"predictor d{n}")
+
+
+def test_train_steps_golden():
+    """Oracle replays 3 iterations of the reference app/vjepa/train.py:main bit-for-bit-ish (fp32)."""
+    g = gold("train_steps.pt")
+    a = g["args"]
+    co = a["optimization"]
+    enc_cfg = dict(patch_size=16, tubelet_size=2, num_heads=1, depth=2, use_rope=True)
+    pred_cfg = dict(num_heads=2, depth=2, use_rope=True, grid_size=4, num_mask_tokens=2, num_patches=64)
+    tr = orc.OracleTrainer(g["init_encoder"], g["init_predictor"], enc_cfg, pred_cfg)
+    ipe = co["ipe"]
+    sched = orc.WarmupCosine(int(co["warmup"] * ipe), co["start_lr"], co["lr"], int(co["ipe_scale"] * co["epochs"] * ipe),
+                             co["final_lr"])
+    wds = orc.CosineWD(co["weight_decay"], int(co["ipe_scale"] * co["epochs"] * ipe), co["final_weight_decay"])
+    for i, s in enumerate(g["samples"]):
+        clips = torch.stack([torch.randn(3, 8, 64, 64, generator=torch.Generator().manual_seed(sd))
+                             for sd in s["clip_seeds"]])
+        assert abs(clips.double().sum().item() - float(s["clip_sum"])) < 1e-6
+        lr, wd = sched.step(), wds.step()
+        assert lr == g["lrs"][i] and wd == g["wds"][i]
+        loss = tr.step(clips, s["enc"], s["pred"], lr, wd, co["ema"][0])
+        assert abs(loss - g["losses"][i]) < 1e-6 * max(1.0, abs(g["losses"][i])), (i, loss, g["losses"][i])
+    for k, v in g["final_encoder"].items():
+        close(tr.enc[k], v, 1e-6, f"final enc {k}")
+    for k, v in g["final_predictor"].items():
+        close(tr.pred[k], v, 1e-6, f"final pred {k}")
+    for k, v in g["final_target"].items():
+        close(tr.tgt[k], v, 1e-6, f"final target {k}")

@@ -23,6 +23,7 @@ SIGNATURES = {
     "vj_get_last_error": [ctypes.c_char_p, ctypes.c_size_t],
     "vj_device_sync": [],
     "vj_gemm_bf16": [_I, _I, _I, _P, _L, _I, _P, _L, _I, _I, _P, _P, _L, _P, _L, _P, _L, _P],
+    "vj_gemm_bf16_splitk": [_I, _I, _I, _P, _L, _I, _P, _L, _I, _I, _P, _P, _L, _P, _L, _P, _L, _I, _P, _L, _P],
     "vj_attn_fwd": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _F, _I, _P, _P, _P],
     "vj_attn_bwd": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _F, _I, _P, _P, _P],
     "vj_layernorm_fwd": [_I, _I, _P, _I, _L, _P, _P, _F, _P, _I, _L, _P, _P, _P],
@@ -36,7 +37,7 @@ SIGNATURES = {
     "vj_add_rows": [_I, _I, _P, _L, _P, _L, _P, _I, _P],
     "vj_pred_index": [_I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P],
     "vj_ids64to32": [_L, _P, _P, _P],
-    "vj_jepa_loss": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _F, _F, _F, _I, _P, _P, _L, _P, _P, _P],
+    "vj_jepa_loss": [_I, _I, _P, _I, _L, _P, _L, _P, _P, _P, _F, _F, _F, _I, _P, _F, _P, _L, _P, _P, _P],
     "vj_check_finite": [_L, _P, _P, _P],
     "vj_adamw": [_L, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, _P, _P],
     "vj_ema": [_L, _P, _P, _F, _P, _P],

@@ -22,7 +22,7 @@
 
 namespace {
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_PARTIAL = 5 };
 
 struct GemmArgs {
   const bf16_t* A;
@@ -36,6 +36,8 @@ struct GemmArgs {
   const float* bias;
   const void* aux;  // EPI_GELU_BWD: bf16 pre-activation; EPI_F32_RESID: f32 residual input
   long ldaux;
+  int kslice;  // split-K: K range of blockIdx.z is [z*kslice, min(K, (z+1)*kslice))
+  float* ws;   // EPI_PARTIAL: f32 partial tiles [splitk][M][N]
 };
 
 constexpr int BM = 128, BN = 128, BK = 64;
@@ -123,17 +125,19 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nk = (g.K + BK - 1) / BK;
-  stage_tile<AK>(ra, g.lda, mleft, 0, g.K, smem, wave, lane);
-  stage_tile<BKM>(rb, g.ldb, nleft, 0, g.K, smem + TILE_BYTES, wave, lane);
+  const int kb = blockIdx.z * g.kslice;
+  const int ke = min(g.K, kb + g.kslice);
+  const int nk = (ke - kb + BK - 1) / BK;
+  stage_tile<AK>(ra, g.lda, mleft, kb, ke, smem, wave, lane);
+  stage_tile<BKM>(rb, g.ldb, nleft, kb, ke, smem + TILE_BYTES, wave, lane);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
       LDS_AS char* nxt = smem + (cur ^ 1) * 2 * TILE_BYTES;
-      stage_tile<AK>(ra, g.lda, mleft, (kt + 1) * BK, g.K, nxt, wave, lane);
-      stage_tile<BKM>(rb, g.ldb, nleft, (kt + 1) * BK, g.K, nxt + TILE_BYTES, wave, lane);
+      stage_tile<AK>(ra, g.lda, mleft, kb + (kt + 1) * BK, ke, nxt, wave, lane);
+      stage_tile<BKM>(rb, g.ldb, nleft, kb + (kt + 1) * BK, ke, nxt + TILE_BYTES, wave, lane);
     }
     const LDS_AS char* As = smem + cur * 2 * TILE_BYTES;
     const LDS_AS char* Bs = As + TILE_BYTES;
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn * 64 + j * 32 + (lane & 31);
     if (n >= g.N) continue;
-    const float bv = g.bias ? g.bias[n] : 0.f;
+    const float bv = (EPI != EPI_PARTIAL && g.bias) ? g.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -164,7 +168,9 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m >= g.M) continue;
         const float v = acc[i][j][r] + bv;
-        if constexpr (EPI == EPI_BF16) {
+        if constexpr (EPI == EPI_PARTIAL) {
+          g.ws[((long)blockIdx.z * g.M + m) * g.N + n] = v;
+        } else if constexpr (EPI == EPI_BF16) {
           ((bf16_t*)g.C)[(long)m * g.ldc + n] = f2bf(v);
         } else if constexpr (EPI == EPI_F32) {
           ((float*)g.C)[(long)m * g.ldc + n] = v;
@@ -184,9 +190,27 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   }
 }
 
+// Split-K combine: C = epilogue(sum_z ws[z]) in fixed z order (deterministic).
+__global__ void k_splitk_reduce(GemmArgs g, int splitk, int epi) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)g.M * g.N;
+  if (i >= total) return;
+  const int m = (int)(i / g.N), n = (int)(i % g.N);
+  float v = g.bias ? g.bias[n] : 0.f;
+  for (int z = 0; z < splitk; ++z) v += g.ws[(long)z * total + i];
+  if (epi == EPI_F32_RESID) {
+    ((float*)g.C)[(long)m * g.ldc + n] = ((const float*)g.aux)[(long)m * g.ldaux + n] + v;
+  } else if (epi == EPI_F32) {
+    ((float*)g.C)[(long)m * g.ldc + n] = v;
+  } else {
+    ((bf16_t*)g.C)[(long)m * g.ldc + n] = f2bf(v);
+  }
+}
+
 template <bool AK, bool BKM>
 int launch_epi(int epi, const GemmArgs& g, dim3 grid, hipStream_t st) {
   switch (epi) {
+    case EPI_PARTIAL: hipLaunchKernelGGL((k_gemm<AK, BKM, EPI_PARTIAL>), grid, dim3(256), 0, st, g); break;
     case EPI_BF16: hipLaunchKernelGGL((k_gemm<AK, BKM, EPI_BF16>), grid, dim3(256), 0, st, g); break;
     case EPI_F32: hipLaunchKernelGGL((k_gemm<AK, BKM, EPI_F32>), grid, dim3(256), 0, st, g); break;
     case EPI_F32_RESID: hipLaunchKernelGGL((k_gemm<AK, BKM, EPI_F32_RESID>), grid, dim3(256), 0, st, g); break;
@@ -200,9 +224,10 @@ int launch_epi(int epi, const GemmArgs& g, dim3 grid, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
-                            int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
-                            void* C2, long ldc2, void* stream) {
+extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B,
+                                   long ldb, int b_kmajor, int epi, const float* bias, const void* aux, long ldaux,
+                                   void* C, long ldc, void* C2, long ldc2, int splitk, float* ws, long ws_floats,
+                                   void* stream) {
   if (M == 0 || N == 0) return VJ_OK;
   VJ_CHECK_ARG(M > 0 && N > 0 && K > 0, "vj_gemm_bf16: bad dims M=%d N=%d K=%d", M, N, K);
   VJ_CHECK_ARG(A && B, "vj_gemm_bf16: null operand");
@@ -218,12 +243,41 @@ extern "C" int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_
   // 32-bit DMA offsets: every operand must span < 2 GB from its tile origin.
   VJ_CHECK_ARG((a_kmajor ? (long)M * lda : (long)K * lda) * 2 < 0x7fffffffL, "vj_gemm_bf16: A too large");
   VJ_CHECK_ARG((b_kmajor ? (long)N * ldb : (long)K * ldb) * 2 < 0x7fffffffL, "vj_gemm_bf16: B too large");
-  GemmArgs g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, C, ldc, C2, ldc2, bias, aux, ldaux};
-  dim3 grid(vj_cdiv(N, BN), vj_cdiv(M, BM));
+  if (splitk < 1) splitk = 1;
+  int kslice = K;
+  if (splitk > 1) {
+    VJ_CHECK_ARG(epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID,
+                 "vj_gemm_bf16_splitk: split-K supports the BF16/F32/F32_RESID epilogues");
+    kslice = vj_cdiv(vj_cdiv(K, splitk), BK) * BK;
+    splitk = vj_cdiv(K, kslice);
+    VJ_CHECK_ARG(ws && ws_floats >= (long)splitk * M * N, "vj_gemm_bf16_splitk: workspace needs %ld floats",
+                 (long)splitk * M * N);
+  }
+  GemmArgs g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, C, ldc, C2, ldc2, bias, aux, ldaux, kslice, ws};
+  dim3 grid(vj_cdiv(N, BN), vj_cdiv(M, BM), splitk);
   VJ_CHECK_ARG(grid.y <= 65535, "vj_gemm_bf16: M too large");
   hipStream_t st = (hipStream_t)stream;
+  if (splitk > 1) {
+    int rc;
+    if (a_kmajor && b_kmajor) rc = launch_epi<true, true>(EPI_PARTIAL, g, grid, st);
+    else if (a_kmajor && !b_kmajor) rc = launch_epi<true, false>(EPI_PARTIAL, g, grid, st);
+    else if (!a_kmajor && b_kmajor) rc = launch_epi<false, true>(EPI_PARTIAL, g, grid, st);
+    else rc = launch_epi<false, false>(EPI_PARTIAL, g, grid, st);
+    if (rc) return rc;
+    const long total = (long)M * N;
+    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, g, splitk, epi);
+    VJ_LAUNCH_CHECK("vj_gemm_bf16_splitk(reduce)");
+    return VJ_OK;
+  }
   if (a_kmajor && b_kmajor) return launch_epi<true, true>(epi, g, grid, st);
   if (a_kmajor && !b_kmajor) return launch_epi<true, false>(epi, g, grid, st);
   if (!a_kmajor && b_kmajor) return launch_epi<false, true>(epi, g, grid, st);
   return launch_epi<false, false>(epi, g, grid, st);
+}
+
+extern "C" int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                            int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
+                            void* C2, long ldc2, void* stream) {
+  return vj_gemm_bf16_splitk(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, epi, bias, aux, ldaux, C, ldc, C2, ldc2, 1,
+                             nullptr, 0, stream);
 }

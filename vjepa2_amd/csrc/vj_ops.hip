@@ -157,19 +157,42 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
 }
 
 // ------------------------------------------------------------------------------------------------
-// Column sums. Stage 1: ws[s][n] = sum over rows in slice s. Stage 2: out[n] (+)= sum_s ws[s][n].
+// Column sums. Stage 1: ws[s][n] = sum over the rows of slice s; thread = 8 consecutive columns
+// (16-B bf16 / 2x16-B f32 loads), 4 row groups per block combined through LDS in fixed order.
 template <bool BF>
-__global__ void k_colsum1(int M, int N, const void* __restrict__ x, long ld, int rows_per_slice, float* __restrict__ ws) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+__global__ __launch_bounds__(256) void k_colsum1(int M, int N, const void* __restrict__ x, long ld, int rows_per_slice,
+                                                 float* __restrict__ ws) {
+  __shared__ float red[4][512];
+  const int cg = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + cg) * 8;
   const long r0 = (long)blockIdx.y * rows_per_slice;
   const long r1 = min((long)M, r0 + rows_per_slice);
-  float s = 0.f;
-  for (long r = r0; r < r1; ++r) {
-    if constexpr (BF) s += bf2f(((const bf16_t*)x)[r * ld + n]);
-    else s += ((const float*)x)[r * ld + n];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c0 < N) {
+    for (long r = r0 + rg; r < r1; r += 4) {
+      if constexpr (BF) {
+        const uint4 u = *(const uint4*)((const bf16_t*)x + r * ld + c0);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[2 * j] += bf2f(w[j] & 0xffff);
+          acc[2 * j + 1] += bf2f(w[j] >> 16);
+        }
+      } else {
+        const float4 a = *(const float4*)((const float*)x + r * ld + c0);
+        const float4 b = *(const float4*)((const float*)x + r * ld + c0 + 4);
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      }
+    }
   }
-  ws[(long)blockIdx.y * N + n] = s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rg][cg * 8 + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int n = blockIdx.x * 512 + i;
+    if (n < N) ws[(long)blockIdx.y * N + n] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+  }
 }
 __global__ void k_colsum2(int S, int N, const float* __restrict__ ws, long ws_ld, float* __restrict__ out, int acc) {
   const int n = blockIdx.x * 256 + threadIdx.x;
@@ -345,8 +368,10 @@ __global__ void k_ids64to32(long n, const long* __restrict__ in, int* __restrict
 struct LossGroups {
   int ngroups;
   int rows[4];
+  float pair_weight;  // 1 / (number of (fpc, mask) pairs averaged by the loss)
 };
-__global__ __launch_bounds__(256) void k_jepa_loss(int R, int D, const float* __restrict__ z, long ldz,
+template <bool ZBF>
+__global__ __launch_bounds__(256) void k_jepa_loss(int R, int D, const void* __restrict__ zp, long ldz,
                                                    const float* __restrict__ tgt, long ldt,
                                                    const int* __restrict__ loss_rows, const float* __restrict__ gamma,
                                                    const float* __restrict__ beta, float eps1, float eps2, float p,
@@ -358,7 +383,7 @@ __global__ __launch_bounds__(256) void k_jepa_loss(int R, int D, const float* __
   int g = 0;
   long acc = lg.rows[0];
   while (g < lg.ngroups - 1 && r >= acc) acc += lg.rows[++g];
-  const float w = 1.f / ((float)lg.rows[g] * (float)D * (float)lg.ngroups);
+  const float w = lg.pair_weight / ((float)lg.rows[g] * (float)D);
   const float* t = tgt + (long)loss_rows[r] * ldt;
   float4 v[LN_MAXV];
   float s = 0.f;
@@ -409,7 +434,13 @@ __global__ __launch_bounds__(256) void k_jepa_loss(int R, int D, const float* __
   for (int i = 0; i < LN_MAXV; ++i) {
     const int c = (i * 64 + lane) * 4;
     if (c < D) {
-      const float4 zv = *(const float4*)(z + r * ldz + c);
+      float4 zv;
+      if constexpr (ZBF) {
+        const uint2 u = *(const uint2*)((const bf16_t*)zp + r * ldz + c);
+        zv = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+      } else {
+        zv = *(const float4*)((const float*)zp + r * ldz + c);
+      }
       const float hv[4] = {(v[i].x - mu) * rs, (v[i].y - mu) * rs, (v[i].z - mu) * rs, (v[i].w - mu) * rs};
       const float zz[4] = {zv.x, zv.y, zv.z, zv.w};
       float gd[4];
@@ -545,7 +576,7 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
 
 extern "C" int vj_layernorm_bwd_blocks(int M) {
   const int b = (M + 3) / 4;
-  return b < 512 ? (b > 0 ? b : 1) : 512;
+  return b < 2048 ? (b > 0 ? b : 1) : 2048;
 }
 
 extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate,
@@ -583,13 +614,14 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
 extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate, float* ws,
                              long ws_floats, void* stream) {
   if (N == 0) return VJ_OK;
-  int S = (M + 255) / 256;
-  if (S > 128) S = 128;
+  VJ_CHECK_ARG(N % 8 == 0 && ld % 8 == 0, "vj_colsum_f32: N and ld must be multiples of 8");
+  int S = (M + 63) / 64;
+  if (S > 256) S = 256;
   if (S < 1) S = 1;
   VJ_CHECK_ARG(ws && ws_floats >= (long)S * N, "vj_colsum_f32: workspace needs %ld floats", (long)S * N);
   const int rps = (M + S - 1) / S;
   hipStream_t st = (hipStream_t)stream;
-  dim3 g1((N + 255) / 256, S);
+  dim3 g1((N + 511) / 512, S);
   if (x_bf16) hipLaunchKernelGGL(k_colsum1<true>, g1, dim3(256), 0, st, M, N, x, ld, rps, ws);
   else hipLaunchKernelGGL(k_colsum1<false>, g1, dim3(256), 0, st, M, N, x, ld, rps, ws);
   hipLaunchKernelGGL(k_colsum2, dim3((N + 255) / 256), dim3(256), 0, st, S, N, ws, (long)N, out, accumulate);
@@ -667,15 +699,16 @@ extern "C" int vj_ids64to32(long n, const long* in, int* out, void* stream) {
   return VJ_OK;
 }
 
-extern "C" int vj_jepa_loss(int R, int D, const float* z, long ldz, const float* tgt, long ldt, const int* loss_rows,
-                            const float* gamma, const float* beta, float eps1, float eps2, float loss_exp,
-                            int ngroups, const int* group_rows, void* dz, long lddz, float* row_loss, float* loss_out,
-                            void* stream) {
+extern "C" int vj_jepa_loss(int R, int D, const void* z, int z_bf16, long ldz, const float* tgt, long ldt,
+                            const int* loss_rows, const float* gamma, const float* beta, float eps1, float eps2,
+                            float loss_exp, int ngroups, const int* group_rows, float pair_weight, void* dz, long lddz,
+                            float* row_loss, float* loss_out, void* stream) {
   if (R == 0) return VJ_OK;
   VJ_CHECK_ARG(D % 4 == 0 && D <= 2048, "vj_jepa_loss: bad D=%d", D);
   VJ_CHECK_ARG(ngroups >= 1 && ngroups <= 4, "vj_jepa_loss: 1..4 groups");
   LossGroups lg{};
   lg.ngroups = ngroups;
+  lg.pair_weight = pair_weight;
   long tot = 0;
   for (int i = 0; i < ngroups; ++i) {
     lg.rows[i] = group_rows[i];
@@ -683,8 +716,12 @@ extern "C" int vj_jepa_loss(int R, int D, const float* z, long ldz, const float*
   }
   VJ_CHECK_ARG(tot == R, "vj_jepa_loss: groups cover %ld rows, R=%d", tot, R);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_jepa_loss, dim3((R + 3) / 4), dim3(256), 0, st, R, D, z, ldz, tgt, ldt, loss_rows, gamma, beta,
-                     eps1, eps2, loss_exp, lg, (bf16_t*)dz, lddz, row_loss);
+  if (z_bf16)
+    hipLaunchKernelGGL(k_jepa_loss<true>, dim3((R + 3) / 4), dim3(256), 0, st, R, D, z, ldz, tgt, ldt, loss_rows, gamma,
+                       beta, eps1, eps2, loss_exp, lg, (bf16_t*)dz, lddz, row_loss);
+  else
+    hipLaunchKernelGGL(k_jepa_loss<false>, dim3((R + 3) / 4), dim3(256), 0, st, R, D, z, ldz, tgt, ldt, loss_rows, gamma,
+                       beta, eps1, eps2, loss_exp, lg, (bf16_t*)dz, lddz, row_loss);
   hipLaunchKernelGGL(k_sum1, dim3(1), dim3(256), 0, st, (long)R, row_loss, loss_out);
   VJ_LAUNCH_CHECK("vj_jepa_loss");
   return VJ_OK;

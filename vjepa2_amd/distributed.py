@@ -1,0 +1,120 @@
+"""Process-group init and bucketed gradient all-reduce (data parallel only, like the reference).
+
+init_distributed follows src/utils/distributed.py:17-51 (env:// rendezvous, "nccl" = RCCL on ROCm,
+fallback to a world of 1). GradReducer replaces the DDP reducer (app/vjepa/train.py:279-281):
+gradients already live in flat arenas ordered by backward readiness, so a bucket is a contiguous
+slice; when the last layer writing into a bucket finishes its backward, the bucket's all-reduce
+(SUM; the 1/world average is folded into the AdamW kernel) is issued asynchronously. With the
+"nccl" backend RCCL runs it on its own HIP stream, ordered after the compute stream's work so far,
+so it overlaps the rest of the backward over xGMI. Buckets are issued strictly in order, so every
+rank issues the same collective sequence.
+"""
+
+import logging
+import os
+
+import torch
+import torch.distributed as dist
+
+logger = logging.getLogger(__name__)
+
+
+def init_distributed(port=37129, rank_and_world_size=(None, None), backend=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    rank, world = rank_and_world_size
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if rank is None or world is None:
+        env = os.environ
+        if "RANK" in env and "WORLD_SIZE" in env:
+            rank, world = int(env["RANK"]), int(env["WORLD_SIZE"])
+        elif "SLURM_NTASKS" in env:
+            rank, world = int(env["SLURM_PROCID"]), int(env["SLURM_NTASKS"])
+        else:
+            return 1, 0
+    if world == 1:
+        return 1, 0
+    try:
+        os.environ.setdefault("MASTER_PORT", str(port))
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl" and torch.cuda.is_available():
+            kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
+        dist.init_process_group(backend=backend, world_size=world, rank=rank, **kw)
+    except Exception as e:  # reference behaviour: fall back to a single process
+        logger.info(f"distributed training not available: {e}")
+        return 1, 0
+    return world, rank
+
+
+class _Bucket:
+    __slots__ = ("view", "pending", "params", "work")
+
+    def __init__(self, view, params):
+        self.view, self.params, self.pending, self.work = view, params, set(), None
+
+
+class GradReducer:
+    """segments: list of (flat_grad_tensor, [(param, offset, numel), ...]) in readiness order.
+    Params of `tail_segments` (tiny no-decay arenas) are reduced as one bucket each at finish()."""
+
+    def __init__(self, segments, tail_segments=(), bucket_mb=64, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.buckets = []
+        cap = int(bucket_mb * (1 << 20)) // 4
+        for flat, plist in segments:
+            cur, lo = [], None
+            for p, off, n in plist:
+                if lo is None:
+                    lo = off
+                cur.append(p)
+                end = off + n
+                if end - lo >= cap:
+                    self.buckets.append(_Bucket(flat[lo:end], cur))
+                    cur, lo = [], None
+            if cur:
+                end = plist[-1][1] + plist[-1][2]
+                self.buckets.append(_Bucket(flat[lo:end], cur))
+        self.tail = [_Bucket(flat[:plist[-1][1] + plist[-1][2]], [p for p, _, _ in plist])
+                     for flat, plist in tail_segments if plist]
+        self.owner = {}
+        for i, b in enumerate(self.buckets):
+            for p in b.params:
+                self.owner[id(p)] = i
+        self.reset()
+
+    def reset(self):
+        for b in self.buckets + self.tail:
+            b.pending = {id(p) for p in b.params}
+            b.work = None
+        self.next = 0
+
+    def _issue(self, b):
+        b.work = dist.all_reduce(b.view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def mark_ready(self, module):
+        """Hook called when `module`'s backward has finished writing its parameter gradients."""
+        for p in module.parameters():
+            i = self.owner.get(id(p))
+            if i is not None:
+                self.buckets[i].pending.discard(id(p))
+        while self.next < len(self.buckets) and not self.buckets[self.next].pending:
+            self._issue(self.buckets[self.next])
+            self.next += 1
+
+    def install(self, modules):
+        for m in modules:
+            m._vj_grad_ready = self.mark_ready
+
+    def finish(self):
+        """Issue what is left (unused params, tails) in order and make the current stream wait."""
+        while self.next < len(self.buckets):
+            self._issue(self.buckets[self.next])
+            self.next += 1
+        for b in self.tail:
+            self._issue(b)
+        for b in self.buckets + self.tail:
+            b.work.wait()
+        self.reset()

@@ -1,0 +1,335 @@
+"""Fused forward/backward of the V-JEPA hot-path layers on the HIP kernels.
+
+Token-major "ragged" execution: the tokens of every sequence of a pass (e.g. both JEPA mask passes
+of a step) are concatenated into one [T, D] buffer; a TokenLayout says where the sequences are
+(attention is the only op that needs it) and which token id each row is (RoPE positions).
+
+The residual stream is kept in f32 (autocast LayerNorm semantics, train.py:438); every GEMM
+operand is bf16 with f32 accumulation. Parameter gradients are accumulated (+=) straight into
+`param.grad` (f32, a view of the flat gradient arena when the trainer owns the parameters), so
+autograd only carries activation gradients between layers.
+"""
+
+import torch
+
+from . import ops
+from .ops import BF16, EPI_BF16, EPI_F32, EPI_F32_RESID, EPI_GELU, F32
+
+# ------------------------------------------------------------------------------------------------
+# parameter views
+
+
+def weight_bf16(p):
+    """bf16 shadow of an f32 parameter: the arena-maintained copy when the trainer owns the
+    parameter (refreshed by the fused AdamW / EMA kernels), else a cached cast keyed by version."""
+    v = getattr(p, "_vj_bf16", None)
+    if v is not None:
+        return v
+    key = (p.data_ptr(), p._version)
+    c = getattr(p, "_vj_bf16_cache", None)
+    if c is None or c[0] != key:
+        c = (key, ops.cast_bf16(p.detach().contiguous()))
+        p._vj_bf16_cache = c
+    return c[1]
+
+
+def grad_buf(p):
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+_ROPE_TABLES = {}
+ROPE_MAX_POS = 512
+
+
+def rope_tables(hd, device):
+    """cos/sin [512, half] of the reference's per-axis angles (modules.py:30-39, fp32 op order)."""
+    key = (hd, str(device))
+    t = _ROPE_TABLES.get(key)
+    if t is None:
+        sw = 2 * ((hd // 3) // 2)
+        omega = torch.arange(sw // 2, dtype=torch.float32)
+        omega /= sw / 2.0
+        omega = 1.0 / 10000**omega
+        freq = torch.arange(ROPE_MAX_POS, dtype=torch.float32)[:, None] * omega[None, :]
+        t = (freq.cos().contiguous().to(device), freq.sin().contiguous().to(device))
+        _ROPE_TABLES[key] = t
+    return t
+
+
+class TokenLayout:
+    """Ragged token batch: `groups` = [(nseq, seqlen), ...] in row order; RoPE ids per row
+    (int32 device tensor) or None for `row % ids_mod`; tokens_per_frame / tokens_per_row."""
+
+    def __init__(self, groups, ids=None, ids_mod=0, tpf=1, tpr=1):
+        self.groups = [(int(n), int(l)) for n, l in groups if n > 0]
+        self.T = sum(n * l for n, l in self.groups)
+        self.ids, self.ids_mod, self.tpf, self.tpr = ids, int(ids_mod), int(tpf), int(tpr)
+
+
+# ------------------------------------------------------------------------------------------------
+# Transformer block (modules.py:500-563): x + attn(LN1 x); x + mlp(LN2 x)
+
+
+def _attn_scale(attn, hd):
+    # F.scaled_dot_product_attention uses the default 1/sqrt(hd) (modules.py:367-372); the non-SDPA
+    # branch uses attn.scale (= qk_scale or hd^-0.5).
+    return hd**-0.5 if attn.use_sdpa else attn.scale
+
+
+def block_forward(x, blk, lay, save):
+    T, D = x.shape
+    attn, mlp = blk.attn, blk.mlp
+    H = attn.num_heads
+    hd = D // H
+    ln1, m1, r1 = ops.layernorm_fwd(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, want_stats=save)
+    qkv = ops.linear_fwd(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
+    if attn.use_rope:
+        c, s = rope_tables(hd, x.device)
+        ops.rope_(qkv, H, hd, 0, D, lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
+    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd))
+    x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32_RESID, resid=x)
+    ln2, m2, r2 = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, want_stats=save)
+    hidden = mlp.fc1.weight.shape[0]
+    pre = torch.empty(T, hidden, dtype=BF16, device=x.device) if save else None
+    _, act = ops.linear_fwd(ln2, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=pre)
+    x_out = ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_F32_RESID, resid=x_mid)
+    saved = (x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, pre, act) if save else None
+    return x_out, saved
+
+
+def _bias_grad(lin, dy):
+    if lin.bias is not None and lin.bias.requires_grad:
+        ops.colsum(dy, grad_buf(lin.bias))
+
+
+def _ln_grads(ln):
+    if ln.weight is None:
+        return None, None
+    return grad_buf(ln.weight), grad_buf(ln.bias)
+
+
+def block_backward(dxo, blk, lay, saved):
+    x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, pre, act = saved
+    attn, mlp = blk.attn, blk.mlp
+    T, D = x.shape
+    H = attn.num_heads
+    hd = D // H
+    dxo_b = ops.cast_bf16(dxo)
+    # MLP
+    dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_pre=pre)
+    ops.linear_wgrad(dxo_b, act, grad_buf(mlp.fc2.weight))
+    _bias_grad(mlp.fc2, dxo)
+    dln2 = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight))
+    ops.linear_wgrad(dpre, ln2, grad_buf(mlp.fc1.weight))
+    _bias_grad(mlp.fc1, dpre)
+    gw, gb = _ln_grads(blk.norm2)
+    dxm, dxm_b = ops.layernorm_bwd(dln2, x_mid, m2, r2, blk.norm2.weight, dres_in=dxo, dweight=gw, dbias=gb,
+                                   want_bf16=True)
+    # attention
+    do = ops.linear_dgrad(dxm_b, weight_bf16(attn.proj.weight))
+    ops.linear_wgrad(dxm_b, o, grad_buf(attn.proj.weight))
+    _bias_grad(attn.proj, dxm)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd))
+    if attn.use_rope:
+        c, s = rope_tables(hd, x.device)
+        ops.rope_(dqkv, H, hd, 0, D, lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s, inverse=True)
+    dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight))
+    ops.linear_wgrad(dqkv, ln1, grad_buf(attn.qkv.weight))
+    _bias_grad(attn.qkv, dqkv)
+    gw, gb = _ln_grads(blk.norm1)
+    dxi, _ = ops.layernorm_bwd(dln1, x, m1, r1, blk.norm1.weight, dres_in=dxm, dweight=gw, dbias=gb)
+    return dxi
+
+
+def _fire_hook(mod):
+    hook = getattr(mod, "_vj_grad_ready", None)
+    if hook is not None:
+        hook(mod)
+
+
+class _BlockFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, blk, lay):
+        y, saved = block_forward(x, blk, lay, save=True)
+        ctx.blk, ctx.lay, ctx.saved = blk, lay, saved
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = block_backward(dy.contiguous(), ctx.blk, ctx.lay, ctx.saved)
+        ctx.saved = None
+        _fire_hook(ctx.blk)
+        return dx, None, None, None
+
+
+def _needs_grad(x, mod):
+    return torch.is_grad_enabled() and (
+        (x is not None and x.requires_grad) or any(p.requires_grad for p in mod.parameters()))
+
+
+def run_block(x, blk, lay):
+    if _needs_grad(x, blk):
+        return _BlockFn.apply(x, blk.norm1.weight, blk, lay)
+    return block_forward(x, blk, lay, save=False)[0]
+
+
+# ------------------------------------------------------------------------------------------------
+# Patch embedding: Conv3d(k=s=(tub,p,p)) over the kept tubelets only (patch_embed.py:42-52 +
+# apply_masks vision_transformer.py:188-192), optional sincos pos-embed add (:183-186).
+
+
+def patch_embed_forward(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0, save=False):
+    proj = pe.proj
+    D = proj.weight.shape[0]
+    kdim = proj.weight[0].numel()
+    p, tub = pe.patch_size, pe.tubelet_size
+    if masks is None:
+        cols = ops.im2col(clip, p, tub)
+    else:
+        B = clip.shape[0]
+        R = sum(B * m.shape[1] for m in masks)
+        cols = torch.empty(R, kdim, dtype=BF16, device=clip.device)
+        r0 = 0
+        for m in masks:
+            n = B * m.shape[1]
+            ops.im2col(clip, p, tub, idx=m.contiguous(), out=cols[r0:r0 + n])
+            r0 += n
+    x = ops.linear_fwd(cols, weight_bf16(proj.weight).view(D, kdim), proj.bias, EPI_F32)
+    if pos_table is not None:
+        ops.add_rows(x, pos_table, idx=pos_ids, idx_mod=pos_mod)
+    return x, (cols if save else None)
+
+
+class _PatchEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, clip, anchor, pe, masks, pos_table, pos_ids, pos_mod):
+        x, cols = patch_embed_forward(clip, pe, masks, pos_table, pos_ids, pos_mod, save=True)
+        ctx.pe, ctx.cols = pe, cols
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        proj = ctx.pe.proj
+        D = proj.weight.shape[0]
+        dx = dx.contiguous()
+        ops.linear_wgrad(ops.cast_bf16(dx), ctx.cols, grad_buf(proj.weight).view(D, -1))
+        _bias_grad(proj, dx)
+        ctx.cols = None
+        _fire_hook(ctx.pe)
+        return None, None, None, None, None, None, None
+
+
+def run_patch_embed(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0):
+    if _needs_grad(None, pe):
+        return _PatchEmbedFn.apply(clip, pe.proj.weight, pe, masks, pos_table, pos_ids, pos_mod)
+    return patch_embed_forward(clip, pe, masks, pos_table, pos_ids, pos_mod)[0]
+
+
+# ------------------------------------------------------------------------------------------------
+# LayerNorm (affine) as its own op (encoder / predictor final norms)
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, ln, out_dtype):
+        y, m, r = ops.layernorm_fwd(x, ln.weight, ln.bias, ln.eps, out_dtype=out_dtype)
+        ctx.ln, ctx.x, ctx.m, ctx.r = ln, x, m, r
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dy_b = dy if dy.dtype == BF16 else ops.cast_bf16(dy)
+        gw, gb = _ln_grads(ctx.ln)
+        dx, _ = ops.layernorm_bwd(dy_b, ctx.x, ctx.m, ctx.r, ctx.ln.weight, dweight=gw, dbias=gb)
+        ctx.x = ctx.m = ctx.r = None
+        _fire_hook(ctx.ln)
+        return dx, None, None, None
+
+
+def run_layernorm(x, ln, out_dtype=F32):
+    if _needs_grad(x, ln):
+        return _LayerNormFn.apply(x, ln.weight, ln, out_dtype)
+    return ops.layernorm_fwd(x, ln.weight, ln.bias, ln.eps, out_dtype=out_dtype, want_stats=False)[0]
+
+
+# ------------------------------------------------------------------------------------------------
+# Linear (predictor_embed / predictor_proj, predictor.py:182, 244)
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, lin, out_dtype):
+        y = ops.linear_fwd(x, weight_bf16(lin.weight), lin.bias, EPI_BF16 if out_dtype == BF16 else EPI_F32)
+        ctx.lin, ctx.x = lin, x
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous()
+        dy_b = dy if dy.dtype == BF16 else ops.cast_bf16(dy)
+        lin = ctx.lin
+        dx = ops.linear_dgrad(dy_b, weight_bf16(lin.weight))
+        ops.linear_wgrad(dy_b, ctx.x, grad_buf(lin.weight))
+        _bias_grad(lin, dy)
+        ctx.x = None
+        _fire_hook(lin)
+        return dx, None, None, None
+
+
+def run_linear(x, lin, out_dtype=F32):
+    """x bf16 [M, K] -> y [M, N] (out_dtype)."""
+    if x.dtype != BF16:
+        x = ops.cast_bf16(x.contiguous())
+    if _needs_grad(x, lin):
+        return _LinearFn.apply(x, lin.weight, lin, out_dtype)
+    return ops.linear_fwd(x, weight_bf16(lin.weight), lin.bias, EPI_BF16 if out_dtype == BF16 else EPI_F32)
+
+
+# ------------------------------------------------------------------------------------------------
+# Predictor token assembly (predictor.py:192-217): context rows scattered to their sorted slots,
+# mask token broadcast into the target slots, optional sincos pos-embed of every slot.
+
+
+class _AssembleFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, e, token, ctx_dst, tgt_rows, S, pos_table, pos_ids, owner):
+        Dp = e.shape[1]
+        seq = torch.empty(S, Dp, dtype=F32, device=e.device)
+        ops.scatter_rows(e, ctx_dst, seq)
+        ops.fill_rows(seq, tgt_rows, token.detach().reshape(-1).contiguous())
+        if pos_table is not None:
+            ops.add_rows(seq, pos_table, idx=pos_ids)
+        ctx.ctx_dst, ctx.tgt_rows, ctx.token, ctx.owner = ctx_dst, tgt_rows, token, owner
+        return seq
+
+    @staticmethod
+    def backward(ctx, dseq):
+        dseq = dseq.contiguous()
+        de = ops.gather_rows(dseq, ctx.ctx_dst)
+        if ctx.token.requires_grad:
+            rows = ops.gather_rows(dseq, ctx.tgt_rows)
+            ops.colsum(rows, grad_buf(ctx.token).view(-1))
+        _fire_hook(ctx.owner)
+        return de, None, None, None, None, None, None, None
+
+
+class _GatherRowsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx):
+        ctx.S, ctx.idx = x.shape[0], idx
+        return ops.gather_rows(x, idx)
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.zeros(ctx.S, dy.shape[1], dtype=dy.dtype, device=dy.device)
+        ops.scatter_rows(dy.contiguous(), ctx.idx, dx)
+        return dx, None
+
+
+def gather_rows(x, idx):
+    if torch.is_grad_enabled() and x.requires_grad:
+        return _GatherRowsFn.apply(x, idx)
+    return ops.gather_rows(x, idx)

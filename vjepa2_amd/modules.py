@@ -1,0 +1,154 @@
+"""Transformer layers with the reference's constructor signatures and parameter names
+(src/models/utils/modules.py): Block, RoPEAttention, Attention, MLP — so state_dict() keys and the
+init-time RNG consumption match the reference exactly. Compute runs on the HIP kernels
+(functions.block_forward / block_backward); these modules are parameter containers plus a
+reference-compatible forward() for direct use.
+"""
+
+import math
+
+import torch
+import torch.nn as nn
+
+from . import functions as fn
+from . import ops
+
+
+class MLP(nn.Module):
+    """modules.py:67-83 (fc1 -> GELU(erf) -> fc2; dropout p=0)."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.0):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.act = act_layer()
+        self.fc2 = nn.Linear(hidden_features, out_features)
+        self.drop = nn.Dropout(drop)
+
+
+class RoPEAttention(nn.Module):
+    """modules.py:261-382: fused QKV, 3-axis RoPE on the (frame, row, col) of each token id, SDPA."""
+
+    use_rope = True
+
+    def __init__(self, dim, num_heads=8, qkv_bias=False, qk_scale=None, attn_drop=0.0, proj_drop=0.0, use_sdpa=True,
+                 grid_size=14, is_causal=False):
+        super().__init__()
+        self.num_heads = num_heads
+        self.head_dim = head_dim = dim // num_heads
+        self.scale = qk_scale or head_dim**-0.5
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop_prob = proj_drop
+        self.proj_drop = nn.Dropout(proj_drop)
+        self.use_sdpa = use_sdpa
+        self.d_dim = self.h_dim = self.w_dim = int(2 * ((head_dim // 3) // 2))
+        self.grid_size = grid_size
+        self.is_causal = is_causal
+        _check_attn(head_dim, attn_drop, proj_drop, is_causal)
+
+    def forward(self, x, mask=None, attn_mask=None, T=None, H_patches=None, W_patches=None):
+        raise NotImplementedError("RoPEAttention runs fused inside Block.forward on the HIP path")
+
+
+class Attention(nn.Module):
+    """modules.py:385-429 (no positional rotation)."""
+
+    use_rope = False
+
+    def __init__(self, dim, num_heads=8, qkv_bias=False, qk_scale=None, attn_drop=0.0, proj_drop=0.0, use_sdpa=True,
+                 is_causal=False):
+        super().__init__()
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        self.scale = qk_scale or head_dim**-0.5
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop_prob = proj_drop
+        self.proj_drop = nn.Dropout(proj_drop)
+        self.use_sdpa = use_sdpa
+        self.is_causal = is_causal
+        _check_attn(head_dim, attn_drop, proj_drop, is_causal)
+
+    def forward(self, x, mask=None, attn_mask=None):
+        raise NotImplementedError("Attention runs fused inside Block.forward on the HIP path")
+
+
+def _check_attn(head_dim, attn_drop, proj_drop, is_causal):
+    if head_dim not in (32, 64):
+        raise NotImplementedError(f"HIP attention supports head_dim 32 and 64 (got {head_dim})")
+    if attn_drop or proj_drop:
+        raise NotImplementedError("attention/projection dropout > 0 is not implemented (configs use 0)")
+    if is_causal:
+        raise NotImplementedError("causal attention is not on the V-JEPA pre-training path")
+
+
+class Block(nn.Module):
+    """modules.py:500-563: x = x + attn(norm1(x)); x = x + mlp(norm2(x))."""
+
+    def __init__(self, dim, num_heads, mlp_ratio=4.0, qkv_bias=False, qk_scale=None, drop=0.0, attn_drop=0.0,
+                 drop_path=0.0, act_layer=nn.GELU, wide_silu=True, norm_layer=nn.LayerNorm, use_sdpa=True,
+                 is_causal=False, grid_size=16, use_rope=False, **kwargs):
+        super().__init__()
+        self.norm1 = norm_layer(dim)
+        if use_rope:
+            self.attn = RoPEAttention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                                      attn_drop=attn_drop, use_sdpa=use_sdpa, is_causal=is_causal,
+                                      grid_size=grid_size, proj_drop=drop)
+        else:
+            self.attn = Attention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                                  attn_drop=attn_drop, use_sdpa=use_sdpa, is_causal=is_causal, proj_drop=drop)
+        if drop_path > 0.0:
+            raise NotImplementedError("stochastic depth (drop_path > 0) is not implemented (configs use 0)")
+        self.drop_path = nn.Identity()
+        self.norm2 = norm_layer(dim)
+        mlp_hidden_dim = int(dim * mlp_ratio)
+        if act_layer is nn.SiLU:
+            raise NotImplementedError("SwiGLU MLP (use_silu) is not implemented on the HIP path (configs use GELU)")
+        self.mlp = MLP(in_features=dim, hidden_features=mlp_hidden_dim, act_layer=act_layer, drop=drop)
+
+    def layout_for(self, B, N, mask, T, H_patches, W_patches, device):
+        g = self.attn.grid_size if self.attn.use_rope else 1
+        if H_patches is None or W_patches is None:
+            tpf, tpr = g * g, g
+        else:
+            tpf, tpr = H_patches * W_patches, W_patches
+        ids = None
+        if mask is not None:
+            ids = ops.ids_to_int32([mask.to(device=device, dtype=torch.int64).contiguous()])
+        return fn.TokenLayout([(B, N)], ids=ids, ids_mod=N, tpf=tpf, tpr=tpr)
+
+    def forward(self, x, mask=None, attn_mask=None, T=None, H_patches=None, W_patches=None):
+        if attn_mask is not None:
+            raise NotImplementedError("attn_mask is not supported on the HIP path")
+        B, N, C = x.shape
+        lay = self.layout_for(B, N, mask, T, H_patches, W_patches, x.device)
+        y = fn.run_block(x.float().reshape(B * N, C).contiguous(), self, lay)
+        return y.reshape(B, N, C)
+
+
+def rescale_blocks(blocks):
+    """vision_transformer.py:147-153 / predictor.py:158-164."""
+    for layer_id, layer in enumerate(blocks):
+        layer.attn.proj.weight.data.div_(math.sqrt(2.0 * (layer_id + 1)))
+        layer.mlp.fc2.weight.data.div_(math.sqrt(2.0 * (layer_id + 1)))
+
+
+def trunc_normal_(tensor, mean=0.0, std=1.0, a=-2.0, b=2.0):
+    """src/utils/tensors.py:14-47 (same RNG consumption: uniform_ then erfinv_)."""
+
+    def norm_cdf(x):
+        return (1.0 + math.erf(x / math.sqrt(2.0))) / 2.0
+
+    with torch.no_grad():
+        lo = norm_cdf((a - mean) / std)
+        hi = norm_cdf((b - mean) / std)
+        tensor.uniform_(2 * lo - 1, 2 * hi - 1)
+        tensor.erfinv_()
+        tensor.mul_(std * math.sqrt(2.0))
+        tensor.add_(mean)
+        tensor.clamp_(min=a, max=b)
+        return tensor

@@ -9,8 +9,48 @@ import torch
 from ._lib import call, int_array
 
 EPI_BF16, EPI_F32, EPI_F32_RESID, EPI_GELU, EPI_GELU_BWD = 0, 1, 2, 3, 4
+EPI_NAMES = ["EPI_BF16", "EPI_F32", "EPI_F32_RESID", "EPI_GELU", "EPI_GELU_BWD"]
 BF16 = torch.bfloat16
 F32 = torch.float32
+
+
+class KernelEvents:
+    """Per-launch HIP-event timing of the library's kernels on the launching (current) stream,
+    with the algorithmic FLOPs of each launch (bench.py roofline). Active only between start/stop."""
+
+    active = None
+
+    def __init__(self):
+        self.rec = []
+
+    def start(self):
+        KernelEvents.active = self
+
+    def stop(self):
+        KernelEvents.active = None
+        torch.cuda.synchronize()
+
+    def summary(self):
+        out = {}
+        for name, flops, s, e in self.rec:
+            d = out.setdefault(name, dict(count=0, total_ms=0.0, flops=0.0))
+            d["count"] += 1
+            d["total_ms"] += s.elapsed_time(e)
+            d["flops"] += flops
+        return out
+
+
+def _call(fn, *args, label=None, flops=0):
+    prof = KernelEvents.active
+    if prof is None:
+        return call(fn, *args)
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    rc = call(fn, *args)
+    e.record()
+    prof.rec.append((label or fn, flops, s, e))
+    return rc
 
 
 def _stream():
@@ -36,14 +76,32 @@ def _rowmajor(t, name):
 # ------------------------------------------------------------------------------------------------
 # GEMMs (nn.Linear forward / dgrad / wgrad)
 def gemm(M, N, K, a, lda, a_kmajor, b, ldb, b_kmajor, epi, out=None, ldc=0, out2=None, ldc2=0, bias=None, aux=None,
-         ldaux=0):
+         ldaux=0, splitk=1):
     _dev(a, b, out, out2, bias, aux)
     if a.dtype != BF16 or b.dtype != BF16:
         raise TypeError("gemm operands must be bf16")
     if bias is not None and (bias.dtype != F32 or bias.numel() < N):
         raise TypeError("gemm bias must be f32 [N]")
-    call("vj_gemm_bf16", M, N, K, _p(a), lda, int(a_kmajor), _p(b), ldb, int(b_kmajor), epi, _p(bias), _p(aux), ldaux,
-         _p(out), ldc, _p(out2), ldc2, _stream())
+    label = f"k_gemm<{int(a_kmajor)},{int(b_kmajor)},{EPI_NAMES[epi]}>"
+    if splitk > 1:  # same slicing as the library: kslice = ceil(ceil(K / splitk) / 64) * 64
+        kslice = (K + splitk - 1) // splitk
+        kslice = (kslice + 63) // 64 * 64
+        splitk = (K + kslice - 1) // kslice
+    if splitk > 1:
+        ws = torch.empty(splitk * M * N, dtype=F32, device=a.device)
+        _call("vj_gemm_bf16_splitk", M, N, K, _p(a), lda, int(a_kmajor), _p(b), ldb, int(b_kmajor), epi, _p(bias),
+              _p(aux), ldaux, _p(out), ldc, _p(out2), ldc2, splitk, _p(ws), ws.numel(), _stream(),
+              label=label + "[splitk]", flops=2.0 * M * N * K)
+        return
+    _call("vj_gemm_bf16", M, N, K, _p(a), lda, int(a_kmajor), _p(b), ldb, int(b_kmajor), epi, _p(bias), _p(aux), ldaux,
+          _p(out), ldc, _p(out2), ldc2, _stream(), label=label, flops=2.0 * M * N * K)
+
+
+def wgrad_splitk(M, N, K, cus=256):
+    """Split K (tokens) until the grid has >= 2 tiles per CU, keeping >= 512 of K per slice."""
+    tiles = -(-M // 128) * -(-N // 128)
+    want = -(-2 * cus // tiles)
+    return max(1, min(want, K // 512))
 
 
 def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
@@ -86,7 +144,7 @@ def linear_wgrad(dy, x, dw):
     K = x.shape[1]
     assert x.shape[0] == M and dw.shape == (N, K) and dw.dtype == F32
     gemm(N, K, M, dy, _rowmajor(dy, "dy"), False, x, _rowmajor(x, "x"), False, EPI_F32_RESID, out=dw,
-         ldc=dw.stride(0), aux=dw, ldaux=dw.stride(0))
+         ldc=dw.stride(0), aux=dw, ldaux=dw.stride(0), splitk=wgrad_splitk(N, K, M))
     return dw
 
 
@@ -95,9 +153,9 @@ def colsum(x, out, accumulate=True):
     """out[n] (+)= sum_m x[m, n]; x bf16 or f32 [M,N]."""
     _dev(x, out)
     M, N = x.shape
-    S = min(128, max(1, (M + 255) // 256))
+    S = min(256, max(1, (M + 63) // 64))
     ws = torch.empty(S * N, dtype=F32, device=x.device)
-    call("vj_colsum_f32", M, N, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(out), int(accumulate), _p(ws),
+    _call("vj_colsum_f32", M, N, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(out), int(accumulate), _p(ws),
          ws.numel(), _stream())
     return out
 
@@ -108,7 +166,7 @@ def layernorm_fwd(x, weight, bias, eps, out_dtype=BF16, want_stats=True):
     y = torch.empty(M, D, dtype=out_dtype, device=x.device)
     mean = torch.empty(M, dtype=F32, device=x.device) if want_stats else None
     rstd = torch.empty(M, dtype=F32, device=x.device) if want_stats else None
-    call("vj_layernorm_fwd", M, D, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(weight), _p(bias), float(eps),
+    _call("vj_layernorm_fwd", M, D, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(weight), _p(bias), float(eps),
          _p(y), int(out_dtype == F32), D, _p(mean), _p(rstd), _stream())
     return y, mean, rstd
 
@@ -128,7 +186,7 @@ def layernorm_bwd(dy, x, mean, rstd, weight, dres_in=None, dweight=None, dbias=N
         nb = load().vj_layernorm_bwd_blocks(M)
         nws = nb * 2 * D
         ws = torch.empty(nws, dtype=F32, device=x.device)
-    call("vj_layernorm_bwd", M, D, _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x"), _p(mean), _p(rstd),
+    _call("vj_layernorm_bwd", M, D, _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x"), _p(mean), _p(rstd),
          _p(weight), _p(dres_in), dres_in.stride(0) if dres_in is not None else 0, _p(dres), D, _p(dres_bf), D,
          _p(dweight), _p(dbias), _p(ws), nws, _stream())
     return dres, dres_bf
@@ -140,7 +198,7 @@ def rope_(qkv, H, hd, q_off, k_off, ids, ids_mod, tpf, tpr, cos_tab, sin_tab, in
     if ids is not None:
         assert ids.dtype == torch.int32 and ids.numel() == T
     half = (hd // 3) // 2
-    call("vj_rope", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, _p(ids), int(ids_mod), int(tpf), int(tpr),
+    _call("vj_rope", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, _p(ids), int(ids_mod), int(tpf), int(tpr),
          _p(cos_tab), _p(sin_tab), half, int(inverse), _stream())
 
 
@@ -155,8 +213,9 @@ def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None):
     o = torch.empty(T, D, dtype=BF16, device=qkv.device)
     stats = torch.empty(2, H, T, dtype=F32, device=qkv.device)
     ns, ln = [g[0] for g in groups], [g[1] for g in groups]
-    call("vj_attn_fwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, v_off, _p(o), D, _p(stats),
-         float(scale), len(groups), int_array(ns), int_array(ln), _stream())
+    _call("vj_attn_fwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, v_off, _p(o), D, _p(stats),
+          float(scale), len(groups), int_array(ns), int_array(ln), _stream(),
+          label=f"attn_fwd<hd{hd}>", flops=sum(4.0 * n * l * l * D for n, l in groups))
     return o, stats
 
 
@@ -166,13 +225,13 @@ def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None):
     D = H * hd
     dqkv = dqkv if dqkv is not None else torch.empty(T, 3 * D, dtype=BF16, device=qkv.device)
     ns, ln = [g[0] for g in groups], [g[1] for g in groups]
-    call("vj_attn_bwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
-         _rowmajor(do, "do"), _p(stats), _p(dqkv), _rowmajor(dqkv, "dqkv"), float(scale), len(groups), int_array(ns),
-         int_array(ln), _stream())
+    _call("vj_attn_bwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
+          _rowmajor(do, "do"), _p(stats), _p(dqkv), _rowmajor(dqkv, "dqkv"), float(scale), len(groups), int_array(ns),
+          int_array(ln), _stream(), label=f"attn_bwd<hd{hd}>", flops=sum(8.0 * n * l * l * D for n, l in groups))
     return dqkv
 
 
-def im2col(clip, patch, tub, idx=None, K=None):
+def im2col(clip, patch, tub, idx=None, out=None):
     """clip f32 [B,C,T,H,W] -> bf16 [R, C*tub*p*p]; idx int64 [B,K] kept tokens (or all tokens)."""
     _dev(clip, idx)
     assert clip.dtype == F32 and clip.is_contiguous()
@@ -180,12 +239,27 @@ def im2col(clip, patch, tub, idx=None, K=None):
     N = (Tf // tub) * (Hf // patch) * (Wf // patch)
     if idx is not None:
         assert idx.dtype == torch.int64 and idx.is_contiguous() and idx.shape[0] == B
+        assert int(idx.shape[1]) <= N
         K = idx.shape[1]
     else:
         K = N
     R = B * K
-    out = torch.empty(R, C * tub * patch * patch, dtype=BF16, device=clip.device)
-    call("vj_im2col_tubelet", R, K, _p(idx), B, C, Tf, Hf, Wf, tub, patch, _p(clip), _p(out), _stream())
+    kdim = C * tub * patch * patch
+    if out is None:
+        out = torch.empty(R, kdim, dtype=BF16, device=clip.device)
+    assert out.shape == (R, kdim) and out.is_contiguous() and out.dtype == BF16
+    _call("vj_im2col_tubelet", R, K, _p(idx), B, C, Tf, Hf, Wf, tub, patch, _p(clip), _p(out), _stream())
+    return out
+
+
+def ids_to_int32(mask_list):
+    """Concatenate int64 [B, K_m] masks (row-major) into one int32 id vector (RoPE positions)."""
+    n = sum(m.numel() for m in mask_list)
+    out = torch.empty(n, dtype=torch.int32, device=mask_list[0].device)
+    o = 0
+    for m in mask_list:
+        ids64to32(m.contiguous(), out=out[o:o + m.numel()])
+        o += m.numel()
     return out
 
 
@@ -195,7 +269,7 @@ def gather_rows(src, idx, out=None, nrows=None):
     R = idx.numel()
     out = out if out is not None else torch.empty(R, src.shape[1], dtype=src.dtype, device=src.device)
     es = src.element_size()
-    call("vj_gather_rows", R, src.shape[1] * es, _p(src), _rowmajor(src, "src") * es, _p(idx), _p(out),
+    _call("vj_gather_rows", R, src.shape[1] * es, _p(src), _rowmajor(src, "src") * es, _p(idx), _p(out),
          _rowmajor(out, "out") * es, 0, _stream())
     return out
 
@@ -205,19 +279,19 @@ def scatter_rows(src, idx, out):
     _dev(src, idx, out)
     R = idx.numel()
     es = src.element_size()
-    call("vj_gather_rows", R, src.shape[1] * es, _p(src), _rowmajor(src, "src") * es, _p(idx), _p(out),
+    _call("vj_gather_rows", R, src.shape[1] * es, _p(src), _rowmajor(src, "src") * es, _p(idx), _p(out),
          _rowmajor(out, "out") * es, 1, _stream())
     return out
 
 
 def fill_rows(dst, idx, vec):
     _dev(dst, idx, vec)
-    call("vj_fill_rows", idx.numel(), dst.shape[1], _p(dst), _rowmajor(dst, "dst"), _p(idx), _p(vec), _stream())
+    _call("vj_fill_rows", idx.numel(), dst.shape[1], _p(dst), _rowmajor(dst, "dst"), _p(idx), _p(vec), _stream())
 
 
 def add_rows(dst, table, idx=None, idx_mod=0):
     _dev(dst, table, idx)
-    call("vj_add_rows", dst.shape[0], dst.shape[1], _p(dst), _rowmajor(dst, "dst"), _p(table),
+    _call("vj_add_rows", dst.shape[0], dst.shape[1], _p(dst), _rowmajor(dst, "dst"), _p(table),
          _rowmajor(table, "table"), _p(idx), int(idx_mod), _stream())
 
 
@@ -226,7 +300,7 @@ def pred_index(mx, my, row0, N, pos, ctx_dst, tgt_rows, loss_rows=None):
     B, K = mx.shape
     Kp = my.shape[1]
     assert mx.dtype == torch.int64 and my.dtype == torch.int64 and mx.is_contiguous() and my.is_contiguous()
-    call("vj_pred_index", B, K, Kp, _p(mx), _p(my), int(row0), B, int(N), _p(pos), _p(ctx_dst), _p(tgt_rows),
+    _call("vj_pred_index", B, K, Kp, _p(mx), _p(my), int(row0), B, int(N), _p(pos), _p(ctx_dst), _p(tgt_rows),
          _p(loss_rows), _stream())
 
 
@@ -234,43 +308,45 @@ def ids64to32(x, out=None):
     _dev(x)
     assert x.dtype == torch.int64 and x.is_contiguous()
     out = out if out is not None else torch.empty(x.numel(), dtype=torch.int32, device=x.device)
-    call("vj_ids64to32", x.numel(), _p(x), _p(out), _stream())
+    _call("vj_ids64to32", x.numel(), _p(x), _p(out), _stream())
     return out
 
 
-def jepa_loss(z, tgt, loss_rows, gamma, beta, group_rows, eps1=1e-6, eps2=1e-5, loss_exp=1.0):
-    """Returns (loss f32 [1], dz bf16 like z, row_loss f32 [R]). z f32 [R, D]."""
+def jepa_loss(z, tgt, loss_rows, gamma, beta, group_rows, eps1=1e-6, eps2=1e-5, loss_exp=1.0, npairs=None):
+    """Returns (loss f32 [1], dz bf16 [R, D], row_loss f32 [R]). z bf16 or f32 [R, D]; the loss is the
+    mean over `npairs` (default len(group_rows)) of each mask group's mean |z - h|^p / p."""
     _dev(z, tgt, loss_rows)
-    assert z.dtype == F32, "jepa_loss: z must be f32"
+    assert z.dtype in (F32, BF16)
     R, D = z.shape
+    npairs = len(group_rows) if npairs is None else npairs
     dz = torch.empty(R, D, dtype=BF16, device=z.device)
     row_loss = torch.empty(R, dtype=F32, device=z.device)
     loss = torch.empty(1, dtype=F32, device=z.device)
-    call("vj_jepa_loss", R, D, _p(z), _rowmajor(z, "z"), _p(tgt), _rowmajor(tgt, "tgt"), _p(loss_rows), _p(gamma),
-         _p(beta), float(eps1), float(eps2), float(loss_exp), len(group_rows), int_array(group_rows), _p(dz), D,
-         _p(row_loss), _p(loss), _stream())
+    _call("vj_jepa_loss", R, D, _p(z), int(z.dtype == BF16), _rowmajor(z, "z"), _p(tgt), _rowmajor(tgt, "tgt"),
+         _p(loss_rows), _p(gamma), _p(beta), float(eps1), float(eps2), float(loss_exp), len(group_rows),
+         int_array(group_rows), 1.0 / npairs, _p(dz), D, _p(row_loss), _p(loss), _stream())
     return loss, dz, row_loss
 
 
 def check_finite(g, found_inf):
     _dev(g, found_inf)
-    call("vj_check_finite", g.numel(), _p(g), _p(found_inf), _stream())
+    _call("vj_check_finite", g.numel(), _p(g), _p(found_inf), _stream())
 
 
 def adamw(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0, found_inf=None):
     _dev(p, g, m, v, p_bf16, found_inf)
-    call("vj_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), float(lr), float(beta1), float(beta2),
+    _call("vj_adamw", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), float(lr), float(beta1), float(beta2),
          float(eps), float(weight_decay), int(step), float(grad_scale), _p(found_inf), _stream())
 
 
 def ema(target, online, momentum, target_bf16=None):
     _dev(target, online, target_bf16)
-    call("vj_ema", target.numel(), _p(target), _p(online), float(momentum), _p(target_bf16), _stream())
+    _call("vj_ema", target.numel(), _p(target), _p(online), float(momentum), _p(target_bf16), _stream())
 
 
 def cast_bf16(x, out=None):
     _dev(x)
     assert x.dtype == F32 and x.is_contiguous()
     out = out if out is not None else torch.empty(x.shape, dtype=BF16, device=x.device)
-    call("vj_cast_bf16", x.numel(), _p(x), _p(out), _stream())
+    _call("vj_cast_bf16", x.numel(), _p(x), _p(out), _stream())
     return out

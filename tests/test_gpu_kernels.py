@@ -29,7 +29,9 @@ def _close(got, exp, atol, rtol, what):
 
 
 # ------------------------------------------------------------------------------------------------
-GEMM_SHAPES = [(128, 128, 64), (300, 136, 72), (264, 200, 1000), (1, 8, 8), (520, 384, 1536)]
+GEMM_SHAPES = [(128, 128, 64), (300, 136, 72), (264, 200, 1000), (1, 8, 8), (520, 384, 1536),
+               # M >= 1024 -> 256-row tile kernel (vj_gemm256.hip): BN=128 ragged, BN=256, K tail, N tail
+               (1100, 384, 1536), (2048, 1024, 200), (1500, 640, 264), (1030, 1160, 128)]
 
 
 @pytest.mark.parametrize("a_kmajor", [True, False])
@@ -81,11 +83,12 @@ def test_gemm_splitk(epi):
     assert torch.equal(out, first), "split-K must be deterministic"
 
 
-def test_gemm_epilogues():
+@pytest.mark.parametrize("M", [333, 1333])
+def test_gemm_epilogues(M):
     from vjepa2_amd import ops
 
     g = torch.Generator(device="cpu").manual_seed(0)
-    M, N, K = 333, 256, 192
+    N, K = 256, 192
     X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
     W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
     b = torch.randn(N, generator=g).to(DEV)

@@ -14,7 +14,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvjepa_hip.so")
-SOURCES = ["vj_capi.hip", "vj_gemm.hip", "vj_attn.hip", "vj_ops.hip"]
+SOURCES = ["vj_capi.hip", "vj_gemm.hip", "vj_gemm256.hip", "vj_attn.hip", "vj_ops.hip"]
 ARCH = os.environ.get("VJEPA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-mcode-object-version=5",

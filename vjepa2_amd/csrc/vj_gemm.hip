@@ -18,6 +18,7 @@
 //   K-major  [128 rows][64 k] (128-B rows): phys chunk = chunk ^ ((row>>1)&7)  -> b128 reads conflict-free
 //   MN-major [64 k][128 rows] (256-B rows): phys chunk = chunk ^ ((k&3)<<2)   -> tr_b16 reads conflict-free
 // Two LDS stages (64 KB) -> 2 workgroups / CU.
+#include <stdlib.h>
 #include "vj_common.h"
 
 namespace {
@@ -224,6 +225,19 @@ int launch_epi(int epi, const GemmArgs& g, dim3 grid, hipStream_t st) {
 
 }  // namespace
 
+int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                        int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
+                        void* C2, long ldc2, hipStream_t st);
+
+static int use_gemm256() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VJ_GEMM256");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v;
+}
+
 extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B,
                                    long ldb, int b_kmajor, int epi, const float* bias, const void* aux, long ldaux,
                                    void* C, long ldc, void* C2, long ldc2, int splitk, float* ws, long ws_floats,
@@ -257,6 +271,11 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
   dim3 grid(vj_cdiv(N, BN), vj_cdiv(M, BM), splitk);
   VJ_CHECK_ARG(grid.y <= 65535, "vj_gemm_bf16: M too large");
   hipStream_t st = (hipStream_t)stream;
+  if (splitk == 1 && M >= 1024 && N >= 128 && use_gemm256()) {
+    const int rc = vj_gemm256_dispatch(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, epi, bias, aux, ldaux, C, ldc, C2,
+                                       ldc2, st);
+    if (rc != VJ_ERR_UNSUPPORTED) return rc;
+  }
   if (splitk > 1) {
     int rc;
     if (a_kmajor && b_kmajor) rc = launch_epi<true, true>(EPI_PARTIAL, g, grid, st);

@@ -1,0 +1,301 @@
+// Large-tile bf16 GEMM for gfx950: 256 x BN x 64 tiles (BN = 256 or 128), 512 threads = 8 waves
+// (2 in M x 4 in N), one workgroup per CU (LDS 128 / 96 KB), v_mfma_f32_16x16x32_bf16.
+// Same operand/epilogue contract as vj_gemm.hip (K-major or MN-major A and B, fused epilogues);
+// used for the forward and data-gradient GEMMs of the encoder / predictor blocks (M = tokens).
+//
+// Schedule (per wave, tile t in LDS slot t&1): 4 phases per K-tile = (k-step, M-half), each
+// 4 x NTN MFMAs on a 64x(BN/4) quarter of the wave tile; the next phase's fragments (16 + 16 VGPRs,
+// double-buffered) are read from LDS while the current phase's MFMAs run, so LDS latency hides under
+// MFMA with 128 accumulator + 64 fragment registers (no spill at 2 waves / SIMD). ONE barrier per
+// tile (before the last phase): it retires this wave's DMA of tile t+1 (issued one tile earlier)
+// and its reads of tile t; tile t+2 is then DMA'd into slot t&1 and stays in flight across it. Epilogue: accumulators staged through LDS (conflict-free padded image) and written as
+// whole 16-B row segments with bias / residual / GELU fused.
+#include "vj_common.h"
+
+namespace {
+
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4 };
+
+struct G256 {
+  const bf16_t* A;
+  const bf16_t* B;
+  int M, N, K;
+  long lda, ldb;
+  void* C;
+  long ldc;
+  void* C2;
+  long ldc2;
+  const float* bias;
+  const void* aux;
+  long ldaux;
+  int tiles_m, tiles_n;
+};
+
+constexpr int BK = 64;
+
+__device__ __forceinline__ uint32_t clampb(long b) {
+  if (b < 0) return 0;
+  return b > 0x7fffffffL ? 0x7fffffffu : (uint32_t)b;
+}
+
+__device__ __forceinline__ int mn_swz(int k) { return 2 * (k & 3) + 8 * ((k >> 3) & 1); }
+
+// K-major image: [ROWS][64] bf16, 128-B rows, chunk ^= (row>>1)&7.
+// MN-major image: [64][ROWS] bf16, ROWS*2-B rows, chunk ^= mn_swz(k).
+template <bool KMAJ, int ROWS>
+__device__ __forceinline__ void stage(__amdgpu_buffer_rsrc_t rs, long ld, int rows_left, int k0, int K,
+                                      LDS_AS char* lds, int wave, int lane) {
+  constexpr int PIECES = ROWS / 8;  // 1-KB DMA pieces per operand tile
+#pragma unroll
+  for (int i = 0; i < PIECES / 8; ++i) {
+    const int p = wave * (PIECES / 8) + i;
+    uint32_t voff;
+    if constexpr (KMAJ) {
+      const int r = p * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      const int kk = k0 + c * 8;
+      voff = (r < rows_left && kk < K) ? (uint32_t)(((long)r * ld + kk) * 2) : VJ_OOB;
+    } else {
+      constexpr int CPR = ROWS / 8;     // chunks per LDS row
+      constexpr int RPP = 64 / CPR;     // k-rows per piece
+      const int kr = p * RPP + lane / CPR;
+      const int c = (lane % CPR) ^ mn_swz(kr);
+      const int col = c * 8;
+      voff = (k0 + kr < K && col < rows_left) ? (uint32_t)(((long)(k0 + kr) * ld + col) * 2) : VJ_OOB;
+    }
+    dma16(rs, lds + p * 1024, voff);
+  }
+}
+
+// 16x16x32 operand fragment: lane l holds X(rb + (l&15), 32s + 8(l>>4) + j), j = 0..7.
+template <bool KMAJ, int ROWS>
+__device__ __forceinline__ bf16x8 frag(const LDS_AS char* lds, int rb, int s, int lane) {
+  if constexpr (KMAJ) {
+    const int r = rb + (lane & 15);
+    const int c = (4 * s + (lane >> 4)) ^ ((r >> 1) & 7);
+    return *(const LDS_AS bf16x8*)(lds + r * 128 + c * 16);
+  } else {
+    const int gi = lane & 15;
+    const int k0 = 32 * s + 8 * (lane >> 4) + (gi >> 2);
+    const int col = rb + 4 * (gi & 3);
+    const int within = (col & 7) * 2;
+    const int c = col >> 3;
+    const s16x4 lo = ds_read_tr16(lds + k0 * (ROWS * 2) + ((c ^ mn_swz(k0)) * 16) + within);
+    const s16x4 hi = ds_read_tr16(lds + (k0 + 4) * (ROWS * 2) + ((c ^ mn_swz(k0 + 4)) * 16) + within);
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// erf with |abs err| <= 1.5e-7 (Abramowitz-Stegun 7.1.26): far below the bf16 rounding of the output.
+__device__ __forceinline__ float erf_fast(float z) {
+  const float a = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float r = 1.f - p * __expf(-a * a);
+  return copysignf(r, z);
+}
+__device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+  return 0.5f * (1.f + erf_fast(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
+template <bool AK, bool BKM, int EPI, int BN>
+__global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
+  constexpr int BM = 256;
+  constexpr int A_BYTES = BM * BK * 2;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int WN = BN / 4;      // wave tile columns (64 / 32)
+  constexpr int NTN = WN / 16;    // 16-wide n tiles per wave (4 / 2)
+  constexpr int NH = NTN / 2;     // n tiles per N-half register set
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  LDS_AS char* smem = (LDS_AS char*)smem_raw;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // XCD-aware bijective remap: each XCD (blocks b % 8) takes a contiguous run of tiles, n fastest.
+  const int nb = g.tiles_m * g.tiles_n;
+  const int b = blockIdx.x, xcd = b & 7, q = nb >> 3, rmd = nb & 7;
+  const int wg = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + (b >> 3);
+  const int tm = wg / g.tiles_n, tn = wg - tm * g.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const bf16_t* abase = AK ? g.A + (long)m0 * g.lda : g.A + m0;
+  const bf16_t* bbase = BKM ? g.B + (long)n0 * g.ldb : g.B + n0;
+  const __amdgpu_buffer_rsrc_t ra =
+      make_rsrc(abase, AK ? clampb((long)(g.M - m0) * g.lda * 2) : clampb(((long)g.K * g.lda - m0) * 2));
+  const __amdgpu_buffer_rsrc_t rb =
+      make_rsrc(bbase, BKM ? clampb((long)(g.N - n0) * g.ldb * 2) : clampb(((long)g.K * g.ldb - n0) * 2));
+  const int mleft = g.M - m0, nleft = g.N - n0;
+  const int nk = (g.K + BK - 1) / BK;
+
+  f32x4 acc[8][NTN];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 Aa[4], Ab[4], Ba[NTN], Bb[NTN];
+
+  auto load_tile = [&](int t) {
+    LDS_AS char* s = smem + (t & 1) * STAGE;
+    stage<AK, BM>(ra, g.lda, mleft, t * BK, g.K, s, wave, lane);
+    stage<BKM, BN>(rb, g.ldb, nleft, t * BK, g.K, s + A_BYTES, wave, lane);
+  };
+  // A fragments of M-half mh (4 m-tiles), k-step ks; B fragments of all NTN n-tiles, k-step ks
+  auto rdA = [&](bf16x8 (&X)[4], int t, int mh, int ks) {
+    const LDS_AS char* s = smem + (t & 1) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) X[i] = frag<AK, BM>(s, wr * 128 + (mh * 4 + i) * 16, ks, lane);
+  };
+  auto rdB = [&](bf16x8 (&Y)[NTN], int t, int ks) {
+    const LDS_AS char* s = smem + (t & 1) * STAGE + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < NTN; ++j) Y[j] = frag<BKM, BN>(s, wc * WN + j * 16, ks, lane);
+  };
+  auto mm = [&](const bf16x8 (&X)[4], int mh, const bf16x8 (&Y)[NTN]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NTN; ++j)
+        acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * 4 + i][j], 0, 0, 0);
+  };
+
+  // prologue: tiles 0 and 1 in flight, then the first fragments (phase 0 of tile 0)
+  load_tile(0);
+  if (nk > 1) load_tile(1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  rdA(Aa, 0, 0, 0);
+  rdB(Ba, 0, 0);
+
+  // Per K-tile t: 4 phases (k-step, M-half) = (0,0) (0,1) (1,0) (1,1), 4*NTN MFMAs each; the
+  // fragments of the NEXT phase are read while the current phase's MFMAs run. One barrier per
+  // tile, before phase 3 (whose prefetch reads tile t+1): it retires this wave's DMA of tile t+1
+  // (issued one tile earlier) and its reads of tile t; then tile t+2 is DMA'd into slot t&1.
+  for (int t = 0; t < nk; ++t) {
+    rdA(Ab, t, 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(Aa, 0, Ba);
+    __builtin_amdgcn_sched_barrier(0);
+    rdA(Aa, t, 0, 1);
+    rdB(Bb, t, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(Ab, 1, Ba);
+    __builtin_amdgcn_sched_barrier(0);
+    rdA(Ab, t, 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(Aa, 0, Bb);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 2 < nk) load_tile(t + 2);
+    if (t + 1 < nk) {
+      rdA(Aa, t + 1, 0, 0);
+      rdB(Ba, t + 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mm(Ab, 1, Bb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  // ---- epilogue: 4 passes of 2 m-tiles (32 rows) per wave through a padded LDS image
+  constexpr int STR = WN + 4;  // floats per staged row (conflict-free ds_write_b32)
+  __syncthreads();
+  LDS_AS float* wl = (LDS_AS float*)(smem + wave * 32 * STR * 4);
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < NTN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          wl[(ii * 16 + (lane >> 4) * 4 + r) * STR + j * 16 + (lane & 15)] = acc[pass * 2 + ii][j][r];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own writes visible to own reads (wave-private)
+    constexpr int LPR = WN / 4;          // lanes per staged row (16-B each)
+    constexpr int RPI = 64 / LPR;        // rows per wave-instruction
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int row = it * RPI + lane / LPR;
+      const int col = (lane % LPR) * 4;
+      const f32x4 v4 = *(const LDS_AS f32x4*)(wl + row * STR + col);
+      const int m = m0 + wr * 128 + pass * 32 + row;
+      const int n = n0 + wc * WN + col;
+      if (m >= g.M || n >= g.N) continue;
+      float v[4] = {v4[0], v4[1], v4[2], v4[3]};
+      if (EPI != EPI_GELU_BWD && g.bias) {
+        const float4 bb = *(const float4*)(g.bias + n);
+        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
+      }
+      if constexpr (EPI == EPI_BF16) {
+        *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+      } else if constexpr (EPI == EPI_F32) {
+        *(float4*)((float*)g.C + (long)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (EPI == EPI_F32_RESID) {
+        const float4 rr = *(const float4*)((const float*)g.aux + (long)m * g.ldaux + n);
+        *(float4*)((float*)g.C + (long)m * g.ldc + n) = make_float4(rr.x + v[0], rr.y + v[1], rr.z + v[2], rr.w + v[3]);
+      } else if constexpr (EPI == EPI_GELU) {
+        const uint32_t p0 = pack_bf2(v[0], v[1]), p1 = pack_bf2(v[2], v[3]);
+        if (g.C) *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(p0, p1);
+        const float x0 = bf2f(p0 & 0xffff), x1 = bf2f(p0 >> 16), x2 = bf2f(p1 & 0xffff), x3 = bf2f(p1 >> 16);
+        *(uint2*)((bf16_t*)g.C2 + (long)m * g.ldc2 + n) =
+            make_uint2(pack_bf2(gelu_fast(x0), gelu_fast(x1)), pack_bf2(gelu_fast(x2), gelu_fast(x3)));
+      } else {  // EPI_GELU_BWD
+        const uint2 pu = *(const uint2*)((const bf16_t*)g.aux + (long)m * g.ldaux + n);
+        const float x0 = bf2f(pu.x & 0xffff), x1 = bf2f(pu.x >> 16), x2 = bf2f(pu.y & 0xffff), x3 = bf2f(pu.y >> 16);
+        *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) =
+            make_uint2(pack_bf2(v[0] * gelu_grad_fast(x0), v[1] * gelu_grad_fast(x1)),
+                       pack_bf2(v[2] * gelu_grad_fast(x2), v[3] * gelu_grad_fast(x3)));
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+}
+
+template <bool AK, bool BKM, int BN>
+int launch256(int epi, const G256& g, hipStream_t st) {
+  dim3 grid(g.tiles_m * g.tiles_n);
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_BF16, BN>), grid, dim3(512), 0, st, g); break;
+    case EPI_F32: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_F32, BN>), grid, dim3(512), 0, st, g); break;
+    case EPI_F32_RESID: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_F32_RESID, BN>), grid, dim3(512), 0, st, g); break;
+    case EPI_GELU: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_GELU, BN>), grid, dim3(512), 0, st, g); break;
+    case EPI_GELU_BWD: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_GELU_BWD, BN>), grid, dim3(512), 0, st, g); break;
+    default: vj_set_error("gemm256: bad epilogue %d", epi); return VJ_ERR_ARG;
+  }
+  VJ_LAUNCH_CHECK("vj_gemm256");
+  return VJ_OK;
+}
+
+}  // namespace
+
+// Called by vj_gemm_bf16_splitk (splitk == 1) when the problem suits a 256-row tile; arguments
+// already validated there. Returns VJ_ERR_UNSUPPORTED when it declines.
+int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                        int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
+                        void* C2, long ldc2, hipStream_t st) {
+  if (epi < EPI_BF16 || epi > EPI_GELU_BWD || N % 8 || ldc % 4 || ldc2 % 4 || ldaux % 4) return VJ_ERR_UNSUPPORTED;
+  if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
+    return VJ_ERR_UNSUPPORTED;
+  const int bn = (N % 256 == 0) ? 256 : 128;
+  G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, C, ldc, C2, ldc2, bias, aux, ldaux,
+         vj_cdiv(M, 256), vj_cdiv(N, bn)};
+  if (bn == 256) {
+    if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
+    if (a_kmajor && !b_kmajor) return launch256<true, false, 256>(epi, g, st);
+    if (!a_kmajor && b_kmajor) return launch256<false, true, 256>(epi, g, st);
+    return launch256<false, false, 256>(epi, g, st);
+  }
+  if (a_kmajor && b_kmajor) return launch256<true, true, 128>(epi, g, st);
+  if (a_kmajor && !b_kmajor) return launch256<true, false, 128>(epi, g, st);
+  if (!a_kmajor && b_kmajor) return launch256<false, true, 128>(epi, g, st);
+  return launch256<false, false, 128>(epi, g, st);
+}

@@ -194,12 +194,21 @@ __global__ __launch_bounds__(256) void k_colsum1(int M, int N, const void* __res
     if (n < N) ws[(long)blockIdx.y * N + n] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
   }
 }
-__global__ void k_colsum2(int S, int N, const float* __restrict__ ws, long ws_ld, float* __restrict__ out, int acc) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+// Stage 2: out[n] (+)= sum_s ws[s][n]; block = 64 columns x 4 row groups, fixed-order LDS combine.
+__global__ __launch_bounds__(256) void k_colsum2(int S, int N, const float* __restrict__ ws, long ws_ld,
+                                                 float* __restrict__ out, int acc) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
   float s = 0.f;
-  for (int i = 0; i < S; ++i) s += ws[(long)i * ws_ld + n];
-  out[n] = acc ? out[n] + s : s;
+  if (n < N)
+    for (int i = rg; i < S; i += 4) s += ws[(long)i * ws_ld + n];
+  red[rg][c] = s;
+  __syncthreads();
+  if (rg == 0 && n < N) {
+    const float t = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    out[n] = acc ? out[n] + t : t;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -576,7 +585,7 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
 
 extern "C" int vj_layernorm_bwd_blocks(int M) {
   const int b = (M + 3) / 4;
-  return b < 2048 ? (b > 0 ? b : 1) : 2048;
+  return b < 1024 ? (b > 0 ? b : 1) : 1024;
 }
 
 extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate,
@@ -604,8 +613,8 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
   VJ_LAUNCH_CHECK("vj_layernorm_bwd");
   if (want_g) {
     // partials laid out [nb][2][D]: dgamma column sums over rows of stride 2D
-    if (dgamma) hipLaunchKernelGGL(k_colsum2, dim3((D + 255) / 256), dim3(256), 0, st, nb, D, ws, 2L * D, dgamma, 1);
-    if (dbeta) hipLaunchKernelGGL(k_colsum2, dim3((D + 255) / 256), dim3(256), 0, st, nb, D, ws + D, 2L * D, dbeta, 1);
+    if (dgamma) hipLaunchKernelGGL(k_colsum2, dim3((D + 63) / 64), dim3(256), 0, st, nb, D, ws, 2L * D, dgamma, 1);
+    if (dbeta) hipLaunchKernelGGL(k_colsum2, dim3((D + 63) / 64), dim3(256), 0, st, nb, D, ws + D, 2L * D, dbeta, 1);
     VJ_LAUNCH_CHECK("vj_layernorm_bwd(reduce)");
   }
   return VJ_OK;
@@ -624,7 +633,7 @@ extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, f
   dim3 g1((N + 511) / 512, S);
   if (x_bf16) hipLaunchKernelGGL(k_colsum1<true>, g1, dim3(256), 0, st, M, N, x, ld, rps, ws);
   else hipLaunchKernelGGL(k_colsum1<false>, g1, dim3(256), 0, st, M, N, x, ld, rps, ws);
-  hipLaunchKernelGGL(k_colsum2, dim3((N + 255) / 256), dim3(256), 0, st, S, N, ws, (long)N, out, accumulate);
+  hipLaunchKernelGGL(k_colsum2, dim3((N + 63) / 64), dim3(256), 0, st, S, N, ws, (long)N, out, accumulate);
   VJ_LAUNCH_CHECK("vj_colsum_f32");
   return VJ_OK;
 }

@@ -58,10 +58,19 @@ int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmaj
 int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o, long ldo,
                 float* stats, float scale, int ngroups, const int* nseq, const int* len, void* stream);
 /* Backward: writes dq/dk/dv (bf16) into dqkv at the same column offsets; uses stats[0] and writes
- * stats[1] = rowsum(dO * O). Deterministic (separate dK/dV and dQ sweeps, no atomics). */
+ * stats[1] = rowsum(dO * O). Deterministic (separate dK/dV and dQ sweeps, no atomics). With cos_t
+ * non-NULL the transpose of the 3-axis RoPE (see vj_rope) is applied to dq and dk before the store,
+ * i.e. dqkv is the gradient w.r.t. the UN-rotated q, k (the QKV projection output). */
 int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, const void* o,
                 long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
-                const int* nseq, const int* len, void* stream);
+                const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
+                const float* cos_t, const float* sin_t, void* stream);
+
+/* Fused QKV projection + RoPE of q and k: C[M, 3*H*hd] (bf16) = A[M,K] W[3*H*hd, K]^T + bias, then
+ * q, k columns rotated (modules.py:330 + 343-365) in the GEMM epilogue. Same RoPE arguments as vj_rope. */
+int vj_qkv_rope_gemm(int M, int K, const void* A, long lda, const void* B, long ldb, const float* bias, void* C,
+                     long ldc, int H, int hd, const int* ids, int ids_mod, int tpf, int tpr, const float* cos_t,
+                     const float* sin_t, void* stream);
 
 /* LayerNorm (nn.LayerNorm / F.layer_norm, modules.py:556-563, train.py:417): x f32 or bf16, y bf16 or f32,
  * gamma/beta optional (both or neither); mean/rstd optional outputs. D % 4 == 0, D <= 2048. */

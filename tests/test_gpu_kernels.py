@@ -230,6 +230,38 @@ def test_rope_fwd_bwd(hd, H):
     _close(buf_d.cpu()[:, :D], q.grad[0].transpose(0, 1).reshape(T, D), 1e-5, 8e-3, "rope inverse")
 
 
+@pytest.mark.parametrize("M", [300, 1500])
+@pytest.mark.parametrize("hd,H", [(64, 2), (32, 3)])
+def test_fused_rope_paths(M, hd, H):
+    """QKV GEMM with fused RoPE == GEMM then rope kernel; attention bwd with fused inverse RoPE ==
+    attention bwd then inverse rope kernel (both within 1 bf16 ulp: the fused path rounds once)."""
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(M + hd)
+    D, K = H * hd, 128
+    tpf, tpr = 16, 4
+    ids = torch.randint(0, 8 * 16, (M,), generator=g).to(DEV).int()
+    cos_t, sin_t = (t.to(DEV) for t in orc.rope_tables(hd, 16))
+    x = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    w = (0.1 * torch.randn(3 * D, K, generator=g)).to(DEV).bfloat16()
+    b = torch.randn(3 * D, generator=g).to(DEV)
+    fused = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
+    ref = (x.float() @ w.float().t() + b).bfloat16()
+    ops.rope_(ref, H, hd, 0, D, ids, 0, tpf, tpr, cos_t, sin_t)
+    _close(fused, ref, 2e-3, 1.6e-2, "qkv_rope")
+    assert torch.equal(fused[:, 2 * D:], ref[:, 2 * D:])
+    # backward
+    groups = [(M // 100, 100)] if M % 100 == 0 else [(1, M)]
+    o, stats = ops.attn_fwd(fused, H, hd, groups, hd ** -0.5)
+    do = torch.randn(M, D, generator=g).to(DEV).bfloat16()
+    st2 = stats.clone()
+    got = ops.attn_bwd(fused, o, do, stats, H, hd, groups, hd ** -0.5, rope=(ids, 0, tpf, tpr, cos_t, sin_t))
+    exp = ops.attn_bwd(fused, o, do, st2, H, hd, groups, hd ** -0.5)
+    ops.rope_(exp, H, hd, 0, D, ids, 0, tpf, tpr, cos_t, sin_t, inverse=True)
+    torch.cuda.synchronize()
+    _close(got, exp, 1e-3, 1.6e-2, "attn_bwd fused inverse rope")
+
+
 # ------------------------------------------------------------------------------------------------
 def test_im2col_patch_embed():
     from vjepa2_amd import ops

@@ -45,7 +45,37 @@ struct AttnArgs {
   int H, T;
   float scale;  // softmax scale (head_dim^-0.5)
   SeqGroups sg;
+  // backward: inverse 3-axis RoPE fused into the dq / dk stores (cos_t == NULL -> none)
+  const int* rope_ids;
+  int rope_mod, rope_tpf, rope_tpr, rope_half;
+  const float* cos_t;
+  const float* sin_t;
 };
+
+// Per-token RoPE positions (frame, row, col) for the inverse rotation (modules.py:293-324).
+struct TokPos {
+  int p[3];
+};
+__device__ __forceinline__ TokPos tok_pos(const AttnArgs& a, int token) {
+  const int id = a.rope_ids ? a.rope_ids[token] : (token % a.rope_mod);
+  const int fr = id / a.rope_tpf;
+  const int hr = (id - a.rope_tpf * fr) / a.rope_tpr;
+  return TokPos{{fr, hr, (id - a.rope_tpf * fr) - a.rope_tpr * hr}};
+}
+// Transpose of rotate_queries_or_keys (modules.py:26-50) on the pair (d, d+1), d even.
+__device__ __forceinline__ void rope_inv(const AttnArgs& a, const TokPos& tp, int d, float& x0, float& x1) {
+  const int sw = 2 * a.rope_half;
+  if (d >= 3 * sw) return;
+  const int ax = d / sw, js = d - ax * sw;
+  const int pos = tp.p[ax];
+  const int f0 = js % a.rope_half, f1 = (js + 1) % a.rope_half;
+  const float c0 = a.cos_t[pos * a.rope_half + f0], s0 = a.sin_t[pos * a.rope_half + f0];
+  const float c1 = a.cos_t[pos * a.rope_half + f1], s1 = a.sin_t[pos * a.rope_half + f1];
+  const float y0 = x0 * c0 + x1 * s1;
+  const float y1 = -x0 * s0 + x1 * c1;
+  x0 = y0;
+  x1 = y1;
+}
 
 // Locate (sequence start, length, tile index in sequence) of a flat tile id.
 __device__ __forceinline__ void locate(const SeqGroups& sg, int tile, int tiles_per_seq_div, int& seq_start,
@@ -362,12 +392,16 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   if (kok) {
     bf16_t* dk = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.k_off + h * HD;
     bf16_t* dv = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.v_off + h * HD;
+    const bool rope = a.cos_t != nullptr;
+    const TokPos tp = rope ? tok_pos(a, seq0 + kloc) : TokPos{{0, 0, 0}};
 #pragma unroll
     for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int col = d * 32 + acc_row(r, lane);
-        *(uint32_t*)(dk + col) = pack_bf2(dkt[d][r] * a.scale, dkt[d][r + 1] * a.scale);
+        float x0 = dkt[d][r] * a.scale, x1 = dkt[d][r + 1] * a.scale;
+        if (rope) rope_inv(a, tp, col, x0, x1);
+        *(uint32_t*)(dk + col) = pack_bf2(x0, x1);
         *(uint32_t*)(dv + col) = pack_bf2(dvt[d][r], dvt[d][r + 1]);
       }
   }
@@ -454,12 +488,16 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   }
   if (qok) {
     bf16_t* dq = a.dqkv + (long)(seq0 + qloc) * a.ldd + a.q_off + h * HD;
+    const bool rope = a.cos_t != nullptr;
+    const TokPos tp = rope ? tok_pos(a, seq0 + qloc) : TokPos{{0, 0, 0}};
 #pragma unroll
     for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int col = d * 32 + acc_row(r, lane);
-        *(uint32_t*)(dq + col) = pack_bf2(dqt[d][r] * a.scale, dqt[d][r + 1] * a.scale);
+        float x0 = dqt[d][r] * a.scale, x1 = dqt[d][r + 1] * a.scale;
+        if (rope) rope_inv(a, tp, col, x0, x1);
+        *(uint32_t*)(dq + col) = pack_bf2(x0, x1);
       }
   }
 }
@@ -519,12 +557,23 @@ extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q
 
 extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
                            const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
-                           float scale, int ngroups, const int* nseq, const int* len, void* stream) {
+                           float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
+                           int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t,
+                           void* stream) {
   if (T == 0) return VJ_OK;
   int rc = check_common(H, hd, ld, ldo);
   if (rc) return rc;
   VJ_CHECK_ARG(lddo % 8 == 0 && ldd % 8 == 0, "vj_attn_bwd: strides must be multiples of 8");
+  VJ_CHECK_ARG(!cos_t || (sin_t && (rope_ids || rope_mod > 0) && rope_tpf > 0 && rope_tpr > 0),
+               "vj_attn_bwd: incomplete RoPE arguments");
   AttnArgs a{};
+  a.rope_ids = rope_ids;
+  a.rope_mod = rope_mod;
+  a.rope_tpf = rope_tpf;
+  a.rope_tpr = rope_tpr;
+  a.rope_half = (hd / 3) / 2;
+  a.cos_t = cos_t;
+  a.sin_t = sin_t;
   a.qkv = (const bf16_t*)qkv; a.ld = ld; a.q_off = q_off; a.k_off = k_off; a.v_off = v_off;
   a.o = (bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.stats = stats;
   a.dqkv = (bf16_t*)dqkv; a.ldd = ldd; a.H = H; a.T = T; a.scale = scale;

@@ -227,7 +227,7 @@ int launch_epi(int epi, const GemmArgs& g, dim3 grid, hipStream_t st) {
 
 int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
                         int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
-                        void* C2, long ldc2, hipStream_t st);
+                        void* C2, long ldc2, hipStream_t st, const void* rope);
 
 static int use_gemm256() {
   static int v = -1;
@@ -273,7 +273,7 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
   hipStream_t st = (hipStream_t)stream;
   if (splitk == 1 && M >= 1024 && N >= 128 && use_gemm256()) {
     const int rc = vj_gemm256_dispatch(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, epi, bias, aux, ldaux, C, ldc, C2,
-                                       ldc2, st);
+                                       ldc2, st, nullptr);
     if (rc != VJ_ERR_UNSUPPORTED) return rc;
   }
   if (splitk > 1) {

@@ -10,11 +10,21 @@
 // tile (before the last phase): it retires this wave's DMA of tile t+1 (issued one tile earlier)
 // and its reads of tile t; tile t+2 is then DMA'd into slot t&1 and stays in flight across it. Epilogue: accumulators staged through LDS (conflict-free padded image) and written as
 // whole 16-B row segments with bias / residual / GELU fused.
+#include <stdlib.h>
 #include "vj_common.h"
 
 namespace {
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5 };
+
+// 3-axis RoPE applied to the q and k columns of a fused QKV projection (modules.py:26-50, 343-365)
+struct RopeP {
+  const int* ids;   // token id per row (NULL -> row % mod)
+  int mod, tpf, tpr;
+  int half, hd, D;  // half = slice/2, head dim, q/k block width (= H * hd)
+  const float* cos_t;
+  const float* sin_t;
+};
 
 struct G256 {
   const bf16_t* A;
@@ -29,7 +39,33 @@ struct G256 {
   const void* aux;
   long ldaux;
   int tiles_m, tiles_n;
+  RopeP rope;
 };
+
+// Rotate 4 consecutive columns n..n+3 (2 adjacent pairs) of token row m in place.
+__device__ __forceinline__ void rope4(const RopeP& r, int m, int n, float* v) {
+  if (n >= 2 * r.D) return;  // v columns untouched
+  const int e0 = (n % r.D) % r.hd;
+  const int sw = 2 * r.half;
+  if (e0 >= 3 * sw) return;
+  const int id = r.ids ? r.ids[m] : (m % r.mod);
+  const int fr = id / r.tpf;
+  const int hr = (id - r.tpf * fr) / r.tpr;
+  const int wc = (id - r.tpf * fr) - r.tpr * hr;
+#pragma unroll
+  for (int j = 0; j < 4; j += 2) {
+    const int e = e0 + j;
+    if (e >= 3 * sw) break;
+    const int ax = e / sw, js = e - ax * sw;
+    const int pos = ax == 0 ? fr : (ax == 1 ? hr : wc);
+    const int f0 = js % r.half, f1 = (js + 1) % r.half;
+    const float c0 = r.cos_t[pos * r.half + f0], s0 = r.sin_t[pos * r.half + f0];
+    const float c1 = r.cos_t[pos * r.half + f1], s1 = r.sin_t[pos * r.half + f1];
+    const float x0 = v[j], x1 = v[j + 1];
+    v[j] = x0 * c0 - x1 * s0;
+    v[j + 1] = x1 * c1 + x0 * s1;
+  }
+}
 
 constexpr int BK = 64;
 
@@ -235,7 +271,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
         const float4 bb = *(const float4*)(g.bias + n);
         v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
       }
-      if constexpr (EPI == EPI_BF16) {
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_ROPE) {
+        if constexpr (EPI == EPI_ROPE) rope4(g.rope, m, n, v);
         *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
       } else if constexpr (EPI == EPI_F32) {
         *(float4*)((float*)g.C + (long)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
@@ -269,6 +306,7 @@ int launch256(int epi, const G256& g, hipStream_t st) {
     case EPI_F32_RESID: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_F32_RESID, BN>), grid, dim3(512), 0, st, g); break;
     case EPI_GELU: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_GELU, BN>), grid, dim3(512), 0, st, g); break;
     case EPI_GELU_BWD: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_GELU_BWD, BN>), grid, dim3(512), 0, st, g); break;
+    case EPI_ROPE: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_ROPE, BN>), grid, dim3(512), 0, st, g); break;
     default: vj_set_error("gemm256: bad epilogue %d", epi); return VJ_ERR_ARG;
   }
   VJ_LAUNCH_CHECK("vj_gemm256");
@@ -281,13 +319,18 @@ int launch256(int epi, const G256& g, hipStream_t st) {
 // already validated there. Returns VJ_ERR_UNSUPPORTED when it declines.
 int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
                         int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
-                        void* C2, long ldc2, hipStream_t st) {
-  if (epi < EPI_BF16 || epi > EPI_GELU_BWD || N % 8 || ldc % 4 || ldc2 % 4 || ldaux % 4) return VJ_ERR_UNSUPPORTED;
+                        void* C2, long ldc2, hipStream_t st, const void* rope) {
+  if (epi < EPI_BF16 || epi > EPI_ROPE || N % 8 || ldc % 4 || ldc2 % 4 || ldaux % 4) return VJ_ERR_UNSUPPORTED;
   if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
     return VJ_ERR_UNSUPPORTED;
   const int bn = (N % 256 == 0) ? 256 : 128;
   G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, C, ldc, C2, ldc2, bias, aux, ldaux,
-         vj_cdiv(M, 256), vj_cdiv(N, bn)};
+         vj_cdiv(M, 256), vj_cdiv(N, bn), RopeP{}};
+  if (epi == EPI_ROPE) {
+    if (!rope) return VJ_ERR_UNSUPPORTED;
+    g.rope = *(const RopeP*)rope;
+    if (g.rope.hd % 4 || g.rope.D % 4) return VJ_ERR_UNSUPPORTED;
+  }
   if (bn == 256) {
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
     if (a_kmajor && !b_kmajor) return launch256<true, false, 256>(epi, g, st);
@@ -298,4 +341,34 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
   if (a_kmajor && !b_kmajor) return launch256<true, false, 128>(epi, g, st);
   if (!a_kmajor && b_kmajor) return launch256<false, true, 128>(epi, g, st);
   return launch256<false, false, 128>(epi, g, st);
+}
+
+extern "C" int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                            int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
+                            void* C2, long ldc2, void* stream);
+extern "C" int vj_rope(int T, int H, int hd, void* qkv, long ld, int q_off, int k_off, const int* ids, int ids_mod,
+                       int tokens_per_frame, int tokens_per_row, const float* cos_tab, const float* sin_tab, int half,
+                       int inverse, void* stream);
+
+// Fused QKV projection + 3-axis RoPE of q and k (modules.py:330 + 343-365): one launch whose epilogue
+// rotates the f32 accumulator rows before the bf16 store; falls back to GEMM + vj_rope for shapes
+// the 256-row kernel declines.
+extern "C" int vj_qkv_rope_gemm(int M, int K, const void* A, long lda, const void* B, long ldb, const float* bias,
+                                void* C, long ldc, int H, int hd, const int* ids, int ids_mod, int tpf, int tpr,
+                                const float* cos_t, const float* sin_t, void* stream) {
+  if (M == 0) return VJ_OK;
+  const int N = 3 * H * hd;
+  VJ_CHECK_ARG(hd % 8 == 0 && cos_t && sin_t && (ids || ids_mod > 0), "vj_qkv_rope_gemm: bad rope arguments");
+  VJ_CHECK_ARG(tpf > 0 && tpr > 0, "vj_qkv_rope_gemm: tokens_per_frame/row must be > 0");
+  const int half = (hd / 3) / 2;
+  const char* e = getenv("VJ_GEMM256");
+  if (M >= 1024 && !(e && e[0] == '0')) {
+    RopeP rp{ids, ids_mod, tpf, tpr, half, hd, H * hd, cos_t, sin_t};
+    const int rc = vj_gemm256_dispatch(M, N, K, A, lda, 1, B, ldb, 1, EPI_ROPE, bias, nullptr, 0, C, ldc, nullptr, 0,
+                                       (hipStream_t)stream, &rp);
+    if (rc != VJ_ERR_UNSUPPORTED) return rc;
+  }
+  int rc = vj_gemm_bf16(M, N, K, A, lda, 1, B, ldb, 1, EPI_BF16, bias, nullptr, 0, C, ldc, nullptr, 0, stream);
+  if (rc) return rc;
+  return vj_rope(M, H, hd, C, ldc, 0, H * hd, ids, ids_mod, tpf, tpr, cos_t, sin_t, half, 0, stream);
 }

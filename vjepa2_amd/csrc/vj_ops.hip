@@ -19,7 +19,7 @@ namespace {
 // LayerNorm forward: wave per row. x f32 or bf16 [M, ldx]; y bf16 or f32 [M, ldy]; optional affine.
 constexpr int LN_MAXV = 8;  // float4 per lane -> D <= 64*4*8 = 2048
 
-template <bool XBF, bool YF32>
+template <bool XBF, bool YF32, int NV>
 __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __restrict__ x, long ldx,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 float eps, void* __restrict__ y, long ldy, float* __restrict__ mean,
@@ -27,10 +27,10 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  float4 v[LN_MAXV];
+  float4 v[NV];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
     if (c < D) {
       if constexpr (XBF) {
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
   const float mu = wave_sum(s) / D;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
     if (c < D) {
       const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
   }
   const float rs = rsqrtf(wave_sum(q) / D + eps);
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) {
+  for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
     if (c < D) {
       float o[4] = {(v[i].x - mu) * rs, (v[i].y - mu) * rs, (v[i].z - mu) * rs, (v[i].w - mu) * rs};
@@ -78,23 +78,23 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
 
 // LayerNorm backward. dy bf16 [M, lddy]; x f32 [M, ldx]; dres f32 [M, ldr] = (dres_in or 0) + dx;
 // optional bf16 copy of the resulting dres; per-block partials of dgamma/dbeta -> ws[blk][2][D].
-template <bool ACC>
+template <bool ACC, int NV>
 __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __restrict__ dy, long lddy,
                                                 const float* __restrict__ x, long ldx, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                 const float* __restrict__ dres_in, long ldri, float* __restrict__ dres,
                                                 long ldr, bf16_t* __restrict__ dres_bf, long ldrb, float* __restrict__ ws) {
-  __shared__ float red[2][LN_MAXV * 256];  // D <= 2048
+  __shared__ float red[2][NV * 256];  // D <= 2048
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float4 dg[LN_MAXV], db[LN_MAXV];
+  float4 dg[NV], db[NV];
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) dg[i] = db[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i = 0; i < NV; ++i) dg[i] = db[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (long row = (long)blockIdx.x * 4 + wave; row < M; row += (long)gridDim.x * 4) {
     const float mu = mean[row], rs = rstd[row];
-    float4 xh[LN_MAXV], g[LN_MAXV];
+    float4 xh[NV], g[NV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = (i * 64 + lane) * 4;
       if (c < D) {
         const float4 xv = *(const float4*)(x + row * ldx + c);
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
     }
     const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
 #pragma unroll
-    for (int i = 0; i < LN_MAXV; ++i) {
+    for (int i = 0; i < NV; ++i) {
       const int c = (i * 64 + lane) * 4;
       if (c < D) {
         float4 dx = make_float4(rs * (g[i].x - m1 - xh[i].x * m2), rs * (g[i].y - m1 - xh[i].y * m2),
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
 #pragma unroll
-      for (int i = 0; i < LN_MAXV; ++i) {
+      for (int i = 0; i < NV; ++i) {
         const int c = (i * 64 + lane) * 4;
         if (c < D) {
           float4* a = (float4*)&red[0][c];
@@ -564,6 +564,11 @@ inline int grid_stride_blocks(long n4) {
 
 }  // namespace
 
+static int ln_nv(int D) {  // float4 per lane for a row of D floats (templated register footprint)
+  const int v = (D + 255) / 256;
+  return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 6 ? 6 : 8;
+}
+
 // ================================================================================================
 // C ABI
 extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma,
@@ -575,10 +580,15 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
   VJ_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "vj_layernorm_fwd: strides must be %%4");
   dim3 grid((M + 3) / 4);
   hipStream_t st = (hipStream_t)stream;
-  if (x_bf16 && y_f32) hipLaunchKernelGGL((k_ln_fwd<true, true>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
-  else if (x_bf16) hipLaunchKernelGGL((k_ln_fwd<true, false>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
-  else if (y_f32) hipLaunchKernelGGL((k_ln_fwd<false, true>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
-  else hipLaunchKernelGGL((k_ln_fwd<false, false>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd);
+  const int nv = ln_nv(D);
+#define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, YF, NVV>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
+#define LNF_NV(XB, YF) switch (nv) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 4: LNF(XB, YF, 4); break; case 6: LNF(XB, YF, 6); break; default: LNF(XB, YF, 8); }
+  if (x_bf16 && y_f32) { LNF_NV(true, true) }
+  else if (x_bf16) { LNF_NV(true, false) }
+  else if (y_f32) { LNF_NV(false, true) }
+  else { LNF_NV(false, false) }
+#undef LNF_NV
+#undef LNF
   VJ_LAUNCH_CHECK("vj_layernorm_fwd");
   return VJ_OK;
 }
@@ -604,12 +614,13 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
   }
   hipStream_t st = (hipStream_t)stream;
   float* part = want_g ? ws : nullptr;
-  if (dres_in)
-    hipLaunchKernelGGL(k_ln_bwd<true>, dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd,
-                       gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part);
-  else
-    hipLaunchKernelGGL(k_ln_bwd<false>, dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd,
-                       gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part);
+  const int nv = ln_nv(D);
+#define LNB(AC, NVV) hipLaunchKernelGGL((k_ln_bwd<AC, NVV>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part)
+#define LNB_NV(AC) switch (nv) { case 1: LNB(AC, 1); break; case 2: LNB(AC, 2); break; case 4: LNB(AC, 4); break; case 6: LNB(AC, 6); break; default: LNB(AC, 8); }
+  if (dres_in) { LNB_NV(true) }
+  else { LNB_NV(false) }
+#undef LNB_NV
+#undef LNB
   VJ_LAUNCH_CHECK("vj_layernorm_bwd");
   if (want_g) {
     // partials laid out [nb][2][D]: dgamma column sums over rows of stride 2D

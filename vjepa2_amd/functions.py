@@ -84,10 +84,12 @@ def block_forward(x, blk, lay, save):
     H = attn.num_heads
     hd = D // H
     ln1, m1, r1 = ops.layernorm_fwd(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, want_stats=save)
-    qkv = ops.linear_fwd(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
-    if attn.use_rope:
+    if attn.use_rope:  # QKV GEMM with RoPE of q, k fused into its epilogue
         c, s = rope_tables(hd, x.device)
-        ops.rope_(qkv, H, hd, 0, D, lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
+        qkv = ops.qkv_rope(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, H, hd, lay.ids, lay.ids_mod, lay.tpf,
+                           lay.tpr, c, s)
+    else:
+        qkv = ops.linear_fwd(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
     o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd))
     x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32_RESID, resid=x)
     ln2, m2, r2 = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, want_stats=save)
@@ -131,10 +133,11 @@ def block_backward(dxo, blk, lay, saved):
     do = ops.linear_dgrad(dxm_b, weight_bf16(attn.proj.weight))
     ops.linear_wgrad(dxm_b, o, grad_buf(attn.proj.weight))
     _bias_grad(attn.proj, dxm)
-    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd))
-    if attn.use_rope:
+    rope = None
+    if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
         c, s = rope_tables(hd, x.device)
-        ops.rope_(dqkv, H, hd, 0, D, lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s, inverse=True)
+        rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope)
     dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight))
     ops.linear_wgrad(dqkv, ln1, grad_buf(attn.qkv.weight))
     _bias_grad(attn.qkv, dqkv)

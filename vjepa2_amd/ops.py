@@ -219,16 +219,32 @@ def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None):
     return o, stats
 
 
-def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None):
+def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None):
+    """rope = (ids, ids_mod, tpf, tpr, cos_tab, sin_tab) -> dq, dk returned w.r.t. the un-rotated q, k."""
     _dev(qkv, o, do, stats)
     T = qkv.shape[0]
     D = H * hd
     dqkv = dqkv if dqkv is not None else torch.empty(T, 3 * D, dtype=BF16, device=qkv.device)
     ns, ln = [g[0] for g in groups], [g[1] for g in groups]
+    ids, mod, tpf, tpr, ct, st = rope if rope is not None else (None, 0, 0, 0, None, None)
     _call("vj_attn_bwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
           _rowmajor(do, "do"), _p(stats), _p(dqkv), _rowmajor(dqkv, "dqkv"), float(scale), len(groups), int_array(ns),
-          int_array(ln), _stream(), label=f"attn_bwd<hd{hd}>", flops=sum(8.0 * n * l * l * D for n, l in groups))
+          int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), _stream(), label=f"attn_bwd<hd{hd}>",
+          flops=sum(8.0 * n * l * l * D for n, l in groups))
     return dqkv
+
+
+def qkv_rope(x, w, bias, H, hd, ids, ids_mod, tpf, tpr, cos_tab, sin_tab):
+    """Fused QKV projection + RoPE of q, k: bf16 [M, 3*H*hd]."""
+    _dev(x, w, bias, ids, cos_tab, sin_tab)
+    M, K = x.shape
+    N = 3 * H * hd
+    assert w.shape == (N, K) and x.dtype == BF16 and w.dtype == BF16
+    out = torch.empty(M, N, dtype=BF16, device=x.device)
+    _call("vj_qkv_rope_gemm", M, K, _p(x), _rowmajor(x, "x"), _p(w), _rowmajor(w, "w"), _p(bias), _p(out), N, H, hd,
+          _p(ids), int(ids_mod), int(tpf), int(tpr), _p(cos_tab), _p(sin_tab), _stream(),
+          label="k_gemm<1,1,EPI_ROPE>", flops=2.0 * M * N * K)
+    return out
 
 
 def im2col(clip, patch, tub, idx=None, out=None):

@@ -54,7 +54,8 @@ int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmaj
  * modules.py:367-372 / 411-418). Tokens of `ngroups` groups of equal-length sequences are
  * concatenated: group g has nseq[g] sequences of len[g] tokens. q/k/v at columns q_off/k_off/v_off
  * + h*hd of the [T, ld] bf16 buffer; O bf16 [T, ldo] at column h*hd.
- * stats: f32 [2][H][T]; forward writes stats[0] = logsumexp (natural log) per (head, token). */
+ * stats: f32 [2][H][T]; forward writes stats[0] = log2-sum-exp2 of the scaled scores in base-2 units
+ * (= logsumexp(scale * s) * log2(e)) per (head, token). */
 int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o, long ldo,
                 float* stats, float scale, int ngroups, const int* nseq, const int* len, void* stream);
 /* Backward: writes dq/dk/dv (bf16) into dqkv at the same column offsets; uses stats[0] and writes
@@ -67,10 +68,11 @@ int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k
                 const float* cos_t, const float* sin_t, void* stream);
 
 /* Fused QKV projection + RoPE of q and k: C[M, 3*H*hd] (bf16) = A[M,K] W[3*H*hd, K]^T + bias, then
- * q, k columns rotated (modules.py:330 + 343-365) in the GEMM epilogue. Same RoPE arguments as vj_rope. */
+ * q, k columns rotated (modules.py:330 + 343-365) in the GEMM epilogue. Same RoPE arguments as vj_rope;
+ * npos = rows of the cos/sin tables, every frame/row/column position of an id must be < npos (<= 1024). */
 int vj_qkv_rope_gemm(int M, int K, const void* A, long lda, const void* B, long ldb, const float* bias, void* C,
                      long ldc, int H, int hd, const int* ids, int ids_mod, int tpf, int tpr, const float* cos_t,
-                     const float* sin_t, void* stream);
+                     const float* sin_t, int npos, void* stream);
 
 /* LayerNorm (nn.LayerNorm / F.layer_norm, modules.py:556-563, train.py:417): x f32 or bf16, y bf16 or f32,
  * gamma/beta optional (both or neither); mean/rstd optional outputs. D % 4 == 0, D <= 2048. */

@@ -17,8 +17,10 @@ LIB = os.path.join(HERE, "libvjepa_hip.so")
 SOURCES = ["vj_capi.hip", "vj_gemm.hip", "vj_gemm256.hip", "vj_attn.hip", "vj_ops.hip"]
 ARCH = os.environ.get("VJEPA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (gfx950 allows it), so the softmax /
+# epilogue VALU reads them in place instead of through v_accvgpr_read/write copies.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-mcode-object-version=5",
-          "-Wno-unused-command-line-argument"]
+          "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wno-unused-command-line-argument"]
 
 
 def _torch_libdir():

@@ -39,7 +39,7 @@ struct AttnArgs {
   long ldo;
   const bf16_t* dout;  // backward: dO
   long lddo;
-  float* stats;  // [2][H][T]: lse (natural log), delta = rowsum(dO*O)
+  float* stats;  // [2][H][T]: lse2 = log2(sum_k 2^(scale*log2e*s_k)), delta = rowsum(dO*O)
   bf16_t* dqkv;  // backward output, same layout as qkv
   long ldd;
   int H, T;
@@ -52,29 +52,53 @@ struct AttnArgs {
   const float* sin_t;
 };
 
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
 // Per-token RoPE positions (frame, row, col) for the inverse rotation (modules.py:293-324).
 struct TokPos {
-  int p[3];
+  int fr, hr, wc;
 };
 __device__ __forceinline__ TokPos tok_pos(const AttnArgs& a, int token) {
   const int id = a.rope_ids ? a.rope_ids[token] : (token % a.rope_mod);
   const int fr = id / a.rope_tpf;
   const int hr = (id - a.rope_tpf * fr) / a.rope_tpr;
-  return TokPos{{fr, hr, (id - a.rope_tpf * fr) - a.rope_tpr * hr}};
+  return TokPos{fr, hr, (id - a.rope_tpf * fr) - a.rope_tpr * hr};
 }
-// Transpose of rotate_queries_or_keys (modules.py:26-50) on the pair (d, d+1), d even.
-__device__ __forceinline__ void rope_inv(const AttnArgs& a, const TokPos& tp, int d, float& x0, float& x1) {
-  const int sw = 2 * a.rope_half;
-  if (d >= 3 * sw) return;
-  const int ax = d / sw, js = d - ax * sw;
-  const int pos = tp.p[ax];
-  const int f0 = js % a.rope_half, f1 = (js + 1) % a.rope_half;
-  const float c0 = a.cos_t[pos * a.rope_half + f0], s0 = a.sin_t[pos * a.rope_half + f0];
-  const float c1 = a.cos_t[pos * a.rope_half + f1], s1 = a.sin_t[pos * a.rope_half + f1];
-  const float y0 = x0 * c0 + x1 * s1;
-  const float y1 = -x0 * s0 + x1 * c1;
-  x0 = y0;
-  x1 = y1;
+// Transpose of rotate_queries_or_keys (modules.py:26-50) applied to the dq / dk rows a lane holds
+// (pairs (d, d+1), d = d0*32 + acc_row(r), r even). The slice width and frequency count follow
+// from HD (half = (HD/3)/2, checked at launch), so the index math is by constants; all table
+// values are loaded before any is used so the loads overlap.
+template <int HD>
+__device__ __forceinline__ void rope_inv_rows(const AttnArgs& a, const TokPos& tp, int lane, f32x16 (&x)[HD / 32]) {
+  constexpr int half = (HD / 3) / 2, sw = 2 * half;
+  float c0[HD / 32][8], s0[HD / 32][8], c1[HD / 32][8], s1[HD / 32][8];
+  const bool hi = lane >= 32;
+  // table index of pair (d, d+1) for a compile-time d (after unrolling): folds to one position
+  auto idx = [&](int d, int o) {
+    if (d >= 3 * sw) return 0;  // inactive pairs read entry 0 and keep their values
+    const int ax = d / sw, js = d - ax * sw;
+    return (ax == 0 ? tp.fr : (ax == 1 ? tp.hr : tp.wc)) * half + (js + o) % half;
+  };
+#pragma unroll
+  for (int d0 = 0; d0 < HD / 32; ++d0)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const int da = d0 * 32 + (r & 3) + 8 * (r >> 2);  // lanes 0-31; lanes 32-63 hold da + 4
+      const int i0 = hi ? idx(da + 4, 0) : idx(da, 0), i1 = hi ? idx(da + 4, 1) : idx(da, 1);
+      c0[d0][r / 2] = a.cos_t[i0];
+      s0[d0][r / 2] = a.sin_t[i0];
+      c1[d0][r / 2] = a.cos_t[i1];
+      s1[d0][r / 2] = a.sin_t[i1];
+    }
+#pragma unroll
+  for (int d0 = 0; d0 < HD / 32; ++d0)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      if (d0 * 32 + acc_row(r, lane) >= 3 * sw) continue;
+      const float x0 = x[d0][r], x1 = x[d0][r + 1];
+      x[d0][r] = x0 * c0[d0][r / 2] + x1 * s1[d0][r / 2];
+      x[d0][r + 1] = -x0 * s0[d0][r / 2] + x1 * c1[d0][r / 2];
+    }
 }
 
 // Locate (sequence start, length, tile index in sequence) of a flat tile id.
@@ -127,7 +151,9 @@ __device__ __forceinline__ bf16x8 row_frag(const LDS_AS char* lds, int rb, int s
   return *(const LDS_AS bf16x8*)(lds + lds_off<HD>(r, 2 * s + (lane >> 5)));
 }
 // Transposed fragment: lane gets X[rows kb+8(j>>2)+4h+(j&3)][col cb + (lane&31)], j = 0..7
-// (the k-permuted order of an accumulator used as an operand).
+// (the k-permuted order of an accumulator used as an operand). Asm reads (ds_read_tr16_async):
+// callers release them with lds_wait() + tie() before use, which lets the next tile's LDS-DMA be
+// issued at the top of the iteration without the compiler serialising the reads behind it.
 template <int HD>
 __device__ __forceinline__ bf16x8 tr_frag(const LDS_AS char* lds, int kb, int cb, int lane) {
   const int h = lane >> 5;
@@ -136,8 +162,8 @@ __device__ __forceinline__ bf16x8 tr_frag(const LDS_AS char* lds, int kb, int cb
   const int r0 = kb + 4 * h + q;
   const int r1 = r0 + 8;
   const int within = (col & 7) * 2;
-  const s16x4 lo = ds_read_tr16(lds + lds_off<HD>(r0, col >> 3) + within);
-  const s16x4 hi = ds_read_tr16(lds + lds_off<HD>(r1, col >> 3) + within);
+  const s16x4 lo = ds_read_tr16_async(lds + lds_off<HD>(r0, col >> 3) + within);
+  const s16x4 hi = ds_read_tr16_async(lds + lds_off<HD>(r1, col >> 3) + within);
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
 }
@@ -160,7 +186,6 @@ __device__ __forceinline__ bf16x8 gload8(const bf16_t* p, bool ok) {
   return *(const bf16x8*)p;
 }
 
-__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 constexpr float LOG2E = 1.4426950408889634f;
 
@@ -192,13 +217,25 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   const __amdgpu_buffer_rsrc_t rk = make_rsrc(kbase, bytes);
   const __amdgpu_buffer_rsrc_t rv = make_rsrc(vbase, bytes);
 
-  f32x16 ot[HD / 32];
+  // O^T accumulators; lt = "ones row" tile: row 0 of V^T replaced by ones gives l = sum_k p (the
+  // softmax denominator of the same bf16 P the numerator uses) on the MFMA pipe instead of 32 adds.
+  f32x16 ot[HD / 32], lt;
 #pragma unroll
-  for (int d = 0; d < HD / 32; ++d)
+  for (int r = 0; r < 16; ++r) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) ot[d][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
+    for (int d = 0; d < HD / 32; ++d) ot[d][r] = 0.f;
+    lt[r] = 0.f;
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)((lane & 31) == 0 ? 1.f : 0.f);
+  // Lazy rescaling: p = exp2(c*s - c*m_use) with m_use the raw-score max seen when O was last
+  // rescaled; O is rescaled (wave-uniform branch) only when some query's max grows by more than
+  // TAU/c, so p <= 2^TAU stays well inside fp32/bf16 range. The result is invariant to m_use.
+  constexpr float TAU = 8.f;
+  float m_use = -INFINITY, cm = 0.f;
   const float c = a.scale * LOG2E;
+  const float tau = TAU / c;
 
   const int nkt = (len + KT - 1) / KT;
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
@@ -206,62 +243,79 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nkt) {
+    const LDS_AS char* Ks = smem + cur * 2 * TB;
+    const LDS_AS char* Vs = Ks + TB;
+    if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
       LDS_AS char* nx = smem + (cur ^ 1) * 2 * TB;
       stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
       stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
     }
-    const LDS_AS char* Ks = smem + cur * 2 * TB;
-    const LDS_AS char* Vs = Ks + TB;
+    // all K fragments first (one LDS wait), then two independent S^T chains interleaved
+    bf16x8 kf[2][HD / 16];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int s = 0; s < HD / 16; ++s) kf[kk][s] = row_frag<HD>(Ks, kk * 32, s, lane);
     f32x16 st[2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
 #pragma unroll
-      for (int s = 0; s < HD / 16; ++s)
-        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Ks, kk * 32, s, lane), qf[s], st[kk], 0, 0, 0);
-    }
-    // mask keys beyond the sequence; tile max
-    float mx = -INFINITY;
+    for (int s = 0; s < HD / 16; ++s)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][s], qf[s], st[kk], 0, 0, 0);
+    // V^T fragments: issued before the softmax so their LDS latency hides under it
+    bf16x8 vf[4][HD / 32];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int d = 0; d < HD / 32; ++d) vf[ks][d] = tr_frag<HD>(Vs, ks * 16, d * 32, lane);
     const int kb = kt * KT;
+    if (kb + KT > len) {  // ragged last tile only: keys beyond the sequence get -inf
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb + kk * 32 + acc_row(r, lane);
-        if (key >= len) st[kk][r] = -INFINITY;
-        mx = fmaxf(mx, st[kk][r]);
-      }
+        for (int r = 0; r < 16; ++r)
+          if (kb + kk * 32 + acc_row(r, lane) >= len) st[kk][r] = -INFINITY;
+    }
+    float mx = st[0][0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, st[0][r]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[1][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f((m_run - m_new) * c);
-    m_run = m_new;
-    float psum = 0.f;
+    if (__builtin_amdgcn_ballot_w64(mx > m_use + tau)) {
+      const float m_new = fmaxf(m_use, mx);
+      const float alpha = __builtin_amdgcn_exp2f((m_use - m_new) * c);
+      m_use = m_new;
+      cm = m_new * c;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+#pragma unroll
+        for (int d = 0; d < HD / 32; ++d) ot[d][r] *= alpha;
+        lt[r] *= alpha;
+      }
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = exp2f((st[kk][r] - m_new) * c);
-        st[kk][r] = p;
-        psum += p;
-      }
-    l_run = l_run * alpha + psum;
-#pragma unroll
-    for (int d = 0; d < HD / 32; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ot[d][r] *= alpha;
+      for (int r = 0; r < 16; ++r) st[kk][r] = __builtin_amdgcn_exp2f(fmaf(st[kk][r], c, -cm));
     // O^T += V^T P^T over 4 key-steps of 16
+    lds_wait();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) tie(vf[ks]);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
 #pragma unroll
-      for (int d = 0; d < HD / 32; ++d)
-        ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<HD>(Vs, ks * 16, d * 32, lane), pf, ot[d], 0, 0, 0);
+      for (int d = 0; d < HD / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
+      lt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf, lt, 0, 0, 0);
     }
     __syncthreads();
   }
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = __shfl(lt[0], lane & 31, 64);  // row 0 of the ones tile lives in lanes 0..31
   const float inv = 1.f / l_tot;
   if (qok) {
     bf16_t* orow = a.o + (long)(seq0 + qloc) * a.ldo + h * HD;
@@ -272,7 +326,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
         const int col = d * 32 + acc_row(r, lane);
         *(uint32_t*)(orow + col) = pack_bf2(ot[d][r] * inv, ot[d][r + 1] * inv);
       }
-    if (hl == 0) a.stats[(long)h * a.T + seq0 + qloc] = m_run * a.scale + logf(l_tot);
+    if (hl == 0) a.stats[(long)h * a.T + seq0 + qloc] = m_use * c + __log2f(l_tot);  // log2 units
   }
 }
 
@@ -351,40 +405,65 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   const int nqt = (len + QT - 1) / QT;
   stage(0, smem);
   __syncthreads();
+  // Rows of queries past the sequence end are zero (DMA range check) with lse2 = delta = 0, so they
+  // add exactly 0 to dV and dK; columns of keys past the end are never stored. No masks needed.
   for (int qt = 0; qt < nqt; ++qt) {
     const int cur = qt & 1;
     if (qt + 1 < nqt) stage(qt + 1, smem + (cur ^ 1) * STAGE);
     const LDS_AS char* Qs = smem + cur * STAGE;
     const LDS_AS char* Ds = Qs + TB;
     const LDS_AS float* Ls = (const LDS_AS float*)(Qs + 2 * TB);
-    // S = Q K^T (rows: queries, col: key)
-    f32x16 sacc, dp;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sacc[r] = dp[r] = 0.f;
+    bf16x8 qa[HD / 16], da[HD / 16];
 #pragma unroll
     for (int s = 0; s < HD / 16; ++s) {
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Qs, 0, s, lane), kf[s], sacc, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Ds, 0, s, lane), vf[s], dp, 0, 0, 0);
+      qa[s] = row_frag<HD>(Qs, 0, s, lane);
+      da[s] = row_frag<HD>(Ds, 0, s, lane);
     }
-    // P = exp(S*scale - lse); dS = P * (dP - delta)
+    // S = Q K^T (rows: queries, col: key); dP - delta = dO V^T - delta (delta as the initial acc)
+    f32x16 sacc, dp;
+    float l2[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = acc_row(r, lane);
-      const bool ok = kok && (qt * QT + qi < len);
-      const float lse = Ls[qi], dl = Ls[32 + qi];
-      const float p = ok ? exp2f(sacc[r] * c - lse * LOG2E) : 0.f;
+      l2[r] = Ls[qi];
+      dp[r] = -Ls[32 + qi];
+      sacc[r] = 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) {
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[s], sacc, 0, 0, 0);
+      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[s], dp, 0, 0, 0);
+    }
+    bf16x8 dtf[2][HD / 32], qtf[2][HD / 32];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int d = 0; d < HD / 32; ++d) {
+        dtf[s2][d] = tr_frag<HD>(Ds, s2 * 16, d * 32, lane);
+        qtf[s2][d] = tr_frag<HD>(Qs, s2 * 16, d * 32, lane);
+      }
+    // P = 2^(c*S - lse2); dS = P * (dP - delta)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -l2[r]));
       sacc[r] = p;
-      dp[r] = p * (dp[r] - dl);
+      dp[r] *= p;
     }
     // dV^T += dO^T P ; dK^T += Q^T dS   (k-permuted accumulators as B operands)
+    lds_wait();
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      tie(dtf[s2]);
+      tie(qtf[s2]);
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       const bf16x8 pf = acc_frag(sacc, s2);
       const bf16x8 sf = acc_frag(dp, s2);
 #pragma unroll
       for (int d = 0; d < HD / 32; ++d) {
-        dvt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<HD>(Ds, s2 * 16, d * 32, lane), pf, dvt[d], 0, 0, 0);
-        dkt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<HD>(Qs, s2 * 16, d * 32, lane), sf, dkt[d], 0, 0, 0);
+        dvt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dtf[s2][d], pf, dvt[d], 0, 0, 0);
+        dkt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtf[s2][d], sf, dkt[d], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -393,15 +472,20 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
     bf16_t* dk = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.k_off + h * HD;
     bf16_t* dv = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.v_off + h * HD;
     const bool rope = a.cos_t != nullptr;
-    const TokPos tp = rope ? tok_pos(a, seq0 + kloc) : TokPos{{0, 0, 0}};
+    const TokPos tp = rope ? tok_pos(a, seq0 + kloc) : TokPos{0, 0, 0};
+    // rotate everything before the first store (the stores could alias the tables, so the
+    // table loads would otherwise be serialised behind them)
+#pragma unroll
+    for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dkt[d][r] *= a.scale;
+    if (rope) rope_inv_rows<HD>(a, tp, lane, dkt);
 #pragma unroll
     for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int col = d * 32 + acc_row(r, lane);
-        float x0 = dkt[d][r] * a.scale, x1 = dkt[d][r + 1] * a.scale;
-        if (rope) rope_inv(a, tp, col, x0, x1);
-        *(uint32_t*)(dk + col) = pack_bf2(x0, x1);
+        *(uint32_t*)(dk + col) = pack_bf2(dkt[d][r], dkt[d][r + 1]);
         *(uint32_t*)(dv + col) = pack_bf2(dvt[d][r], dvt[d][r + 1]);
       }
   }
@@ -431,7 +515,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
     qf[s] = gload8(qrow + 16 * s + 8 * hl, qok);
     gf[s] = gload8(grow + 16 * s + 8 * hl, qok);
   }
-  const float lse2 = qok ? a.stats[(long)h * a.T + seq0 + qloc] * LOG2E : 0.f;
+  const float lse2 = qok ? a.stats[(long)h * a.T + seq0 + qloc] : 0.f;
   const float dl = qok ? a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc] : 0.f;
 
   const uint32_t bytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
@@ -451,37 +535,65 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nkt) {
+    const LDS_AS char* Ks = smem + cur * 2 * TB;
+    const LDS_AS char* Vs = Ks + TB;
+    if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
       LDS_AS char* nx = smem + (cur ^ 1) * 2 * TB;
       stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
       stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
     }
-    const LDS_AS char* Ks = smem + cur * 2 * TB;
-    const LDS_AS char* Vs = Ks + TB;
+    bf16x8 ka[2][HD / 16], va[2][HD / 16], ktf[2][2][HD / 32];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      f32x16 st, dpt;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st[r] = dpt[r] = 0.f;
 #pragma unroll
       for (int s = 0; s < HD / 16; ++s) {
-        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Ks, kk * 32, s, lane), qf[s], st, 0, 0, 0);
-        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag<HD>(Vs, kk * 32, s, lane), gf[s], dpt, 0, 0, 0);
+        ka[kk][s] = row_frag<HD>(Ks, kk * 32, s, lane);
+        va[kk][s] = row_frag<HD>(Vs, kk * 32, s, lane);
       }
 #pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int d = 0; d < HD / 32; ++d) ktf[kk][s2][d] = tr_frag<HD>(Ks, kk * 32 + s2 * 16, d * 32, lane);
+    }
+    // keys past the end are zero rows of K and V; masked on the ragged last tile only so an extreme
+    // lse cannot turn 2^(-lse2) * 0 into inf * 0
+    const bool ragged = (kt + 1) * KT > len;
+    f32x16 st[2], dpt[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int key = kt * KT + kk * 32 + acc_row(r, lane);
-        const bool ok = qok && key < len;
-        const float p = ok ? exp2f(st[r] * c - lse2) : 0.f;
-        dpt[r] = p * (dpt[r] - dl);
+        st[kk][r] = 0.f;
+        dpt[kk][r] = -dl;
+      }
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][s], qf[s], st[kk], 0, 0, 0);
+        dpt[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[kk][s], gf[s], dpt[kk], 0, 0, 0);
+      }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = __builtin_amdgcn_exp2f(fmaf(st[kk][r], c, -lse2));
+        if (ragged && kt * KT + kk * 32 + acc_row(r, lane) >= len) p = 0.f;
+        dpt[kk][r] *= p;
+      }
+      if (kk == 0) {
+        lds_wait();
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) tie(ktf[k2][s2]);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 sf = acc_frag(dpt, s2);
+        const bf16x8 sf = acc_frag(dpt[kk], s2);
 #pragma unroll
         for (int d = 0; d < HD / 32; ++d)
-          dqt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag<HD>(Ks, kk * 32 + s2 * 16, d * 32, lane), sf,
-                                                           dqt[d], 0, 0, 0);
+          dqt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktf[kk][s2][d], sf, dqt[d], 0, 0, 0);
       }
     }
     __syncthreads();
@@ -489,16 +601,17 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   if (qok) {
     bf16_t* dq = a.dqkv + (long)(seq0 + qloc) * a.ldd + a.q_off + h * HD;
     const bool rope = a.cos_t != nullptr;
-    const TokPos tp = rope ? tok_pos(a, seq0 + qloc) : TokPos{{0, 0, 0}};
+    const TokPos tp = rope ? tok_pos(a, seq0 + qloc) : TokPos{0, 0, 0};
 #pragma unroll
     for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int col = d * 32 + acc_row(r, lane);
-        float x0 = dqt[d][r] * a.scale, x1 = dqt[d][r + 1] * a.scale;
-        if (rope) rope_inv(a, tp, col, x0, x1);
-        *(uint32_t*)(dq + col) = pack_bf2(x0, x1);
-      }
+      for (int r = 0; r < 16; ++r) dqt[d][r] *= a.scale;
+    if (rope) rope_inv_rows<HD>(a, tp, lane, dqt);  // rotate first, then store (see k_attn_bwd_dkdv)
+#pragma unroll
+    for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2)
+        *(uint32_t*)(dq + d * 32 + acc_row(r, lane)) = pack_bf2(dqt[d][r], dqt[d][r + 1]);
   }
 }
 

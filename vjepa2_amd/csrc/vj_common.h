@@ -12,6 +12,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short bf16_t;  // storage type of a bf16 element in global memory
 
 #define LDS_AS __attribute__((address_space(3)))
@@ -77,6 +78,22 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, LDS_AS void* lds
 
 __device__ __forceinline__ s16x4 ds_read_tr16(const LDS_AS void* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s16x4*)p);
+}
+// The same read as inline asm. The compiler's wait-count pass treats the builtin as a possible
+// reader of in-flight LDS-DMA data and puts an s_waitcnt vmcnt(0) before it, which serialises the
+// next tile's DMA with the current tile's reads. The asm form is invisible to that pass: its result
+// must be released with lds_wait() + tie() before use.
+__device__ __forceinline__ s16x4 ds_read_tr16_async(const LDS_AS void* p) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"((uint32_t)(uintptr_t)p) : "memory");
+  return r;
+}
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Orders every later use of x after the preceding lds_wait() (volatile asm keeps program order).
+template <typename T, int N>
+__device__ __forceinline__ void tie(T (&x)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(x[i]));
 }
 
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }

@@ -191,6 +191,27 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   }
 }
 
+// Split-K combine, 4 columns per thread (N % 4 == 0): C = epilogue(sum_z ws[z]) in fixed z order.
+__global__ void k_splitk_reduce4(GemmArgs g, int splitk, int epi) {
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  const long total = (long)g.M * g.N;
+  if (i >= total) return;
+  const int m = (int)(i / g.N), n = (int)(i % g.N);
+  float4 v = g.bias ? *(const float4*)(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z = 0; z < splitk; ++z) {
+    const float4 w = *(const float4*)(g.ws + (long)z * total + i);
+    v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+  }
+  if (epi == EPI_F32_RESID) {
+    const float4 r = *(const float4*)((const float*)g.aux + (long)m * g.ldaux + n);
+    *(float4*)((float*)g.C + (long)m * g.ldc + n) = make_float4(r.x + v.x, r.y + v.y, r.z + v.z, r.w + v.w);
+  } else if (epi == EPI_F32) {
+    *(float4*)((float*)g.C + (long)m * g.ldc + n) = v;
+  } else {
+    *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(pack_bf2(v.x, v.y), pack_bf2(v.z, v.w));
+  }
+}
+
 // Split-K combine: C = epilogue(sum_z ws[z]) in fixed z order (deterministic).
 __global__ void k_splitk_reduce(GemmArgs g, int splitk, int epi) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -225,6 +246,8 @@ int launch_epi(int epi, const GemmArgs& g, dim3 grid, hipStream_t st) {
 
 }  // namespace
 
+int vj_gemm256_partial(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                       int b_kmajor, int kslice, int splitk, float* ws, hipStream_t st);
 int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
                         int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
                         void* C2, long ldc2, hipStream_t st, const void* rope);
@@ -277,14 +300,23 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
     if (rc != VJ_ERR_UNSUPPORTED) return rc;
   }
   if (splitk > 1) {
-    int rc;
-    if (a_kmajor && b_kmajor) rc = launch_epi<true, true>(EPI_PARTIAL, g, grid, st);
-    else if (a_kmajor && !b_kmajor) rc = launch_epi<true, false>(EPI_PARTIAL, g, grid, st);
-    else if (!a_kmajor && b_kmajor) rc = launch_epi<false, true>(EPI_PARTIAL, g, grid, st);
-    else rc = launch_epi<false, false>(EPI_PARTIAL, g, grid, st);
+    int rc = VJ_ERR_UNSUPPORTED;
+    if (use_gemm256())
+      rc = vj_gemm256_partial(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, kslice, splitk, ws, st);
+    if (rc == VJ_ERR_UNSUPPORTED) {
+      if (a_kmajor && b_kmajor) rc = launch_epi<true, true>(EPI_PARTIAL, g, grid, st);
+      else if (a_kmajor && !b_kmajor) rc = launch_epi<true, false>(EPI_PARTIAL, g, grid, st);
+      else if (!a_kmajor && b_kmajor) rc = launch_epi<false, true>(EPI_PARTIAL, g, grid, st);
+      else rc = launch_epi<false, false>(EPI_PARTIAL, g, grid, st);
+    }
     if (rc) return rc;
     const long total = (long)M * N;
-    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, g, splitk, epi);
+    const bool vec = N % 4 == 0 && ldc % 4 == 0 && (epi != EPI_F32_RESID || ldaux % 4 == 0) &&
+                     ((uintptr_t)C & 15) == 0 && ((uintptr_t)aux & 15) == 0 && ((uintptr_t)bias & 15) == 0;
+    if (vec)
+      hipLaunchKernelGGL(k_splitk_reduce4, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, st, g, splitk, epi);
+    else
+      hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, g, splitk, epi);
     VJ_LAUNCH_CHECK("vj_gemm_bf16_splitk(reduce)");
     return VJ_OK;
   }

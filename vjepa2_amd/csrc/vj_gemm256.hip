@@ -15,7 +15,7 @@
 
 namespace {
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5, EPI_PARTIAL = 6 };
 
 // 3-axis RoPE applied to the q and k columns of a fused QKV projection (modules.py:26-50, 343-365)
 struct RopeP {
@@ -24,6 +24,7 @@ struct RopeP {
   int half, hd, D;  // half = slice/2, head dim, q/k block width (= H * hd)
   const float* cos_t;
   const float* sin_t;
+  int npos;         // table rows (positions); every position of every id is < npos <= 1024
 };
 
 struct G256 {
@@ -40,32 +41,9 @@ struct G256 {
   long ldaux;
   int tiles_m, tiles_n;
   RopeP rope;
+  int kslice;  // EPI_PARTIAL: blockIdx.y = K slice z covers [z*kslice, min(K, (z+1)*kslice))
+  float* ws;   // EPI_PARTIAL: f32 partial products [splitk][M][N]
 };
-
-// Rotate 4 consecutive columns n..n+3 (2 adjacent pairs) of token row m in place.
-__device__ __forceinline__ void rope4(const RopeP& r, int m, int n, float* v) {
-  if (n >= 2 * r.D) return;  // v columns untouched
-  const int e0 = (n % r.D) % r.hd;
-  const int sw = 2 * r.half;
-  if (e0 >= 3 * sw) return;
-  const int id = r.ids ? r.ids[m] : (m % r.mod);
-  const int fr = id / r.tpf;
-  const int hr = (id - r.tpf * fr) / r.tpr;
-  const int wc = (id - r.tpf * fr) - r.tpr * hr;
-#pragma unroll
-  for (int j = 0; j < 4; j += 2) {
-    const int e = e0 + j;
-    if (e >= 3 * sw) break;
-    const int ax = e / sw, js = e - ax * sw;
-    const int pos = ax == 0 ? fr : (ax == 1 ? hr : wc);
-    const int f0 = js % r.half, f1 = (js + 1) % r.half;
-    const float c0 = r.cos_t[pos * r.half + f0], s0 = r.sin_t[pos * r.half + f0];
-    const float c1 = r.cos_t[pos * r.half + f1], s1 = r.sin_t[pos * r.half + f1];
-    const float x0 = v[j], x1 = v[j + 1];
-    v[j] = x0 * c0 - x1 * s0;
-    v[j + 1] = x1 * c1 + x0 * s1;
-  }
-}
 
 constexpr int BK = 64;
 
@@ -116,8 +94,8 @@ __device__ __forceinline__ bf16x8 frag(const LDS_AS char* lds, int rb, int s, in
     const int col = rb + 4 * (gi & 3);
     const int within = (col & 7) * 2;
     const int c = col >> 3;
-    const s16x4 lo = ds_read_tr16(lds + k0 * (ROWS * 2) + ((c ^ mn_swz(k0)) * 16) + within);
-    const s16x4 hi = ds_read_tr16(lds + (k0 + 4) * (ROWS * 2) + ((c ^ mn_swz(k0 + 4)) * 16) + within);
+    const s16x4 lo = ds_read_tr16_async(lds + k0 * (ROWS * 2) + ((c ^ mn_swz(k0)) * 16) + within);
+    const s16x4 hi = ds_read_tr16_async(lds + (k0 + 4) * (ROWS * 2) + ((c ^ mn_swz(k0 + 4)) * 16) + within);
     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
   }
@@ -163,14 +141,17 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
   const int tm = wg / g.tiles_n, tn = wg - tm * g.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const bf16_t* abase = AK ? g.A + (long)m0 * g.lda : g.A + m0;
-  const bf16_t* bbase = BKM ? g.B + (long)n0 * g.ldb : g.B + n0;
-  const __amdgpu_buffer_rsrc_t ra =
-      make_rsrc(abase, AK ? clampb((long)(g.M - m0) * g.lda * 2) : clampb(((long)g.K * g.lda - m0) * 2));
-  const __amdgpu_buffer_rsrc_t rb =
-      make_rsrc(bbase, BKM ? clampb((long)(g.N - n0) * g.ldb * 2) : clampb(((long)g.K * g.ldb - n0) * 2));
+  // split-K (EPI_PARTIAL): this block's K range starts at kb; Keff = its length
+  const int kb = EPI == EPI_PARTIAL ? (int)blockIdx.y * g.kslice : 0;
+  const int Keff = EPI == EPI_PARTIAL ? min(g.K, kb + g.kslice) - kb : g.K;
+  const bf16_t* abase = AK ? g.A + (long)m0 * g.lda + kb : g.A + (long)kb * g.lda + m0;
+  const bf16_t* bbase = BKM ? g.B + (long)n0 * g.ldb + kb : g.B + (long)kb * g.ldb + n0;
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(
+      abase, AK ? clampb((long)(g.M - m0) * g.lda * 2 - kb * 2L) : clampb(((long)(g.K - kb) * g.lda - m0) * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(
+      bbase, BKM ? clampb((long)(g.N - n0) * g.ldb * 2 - kb * 2L) : clampb(((long)(g.K - kb) * g.ldb - n0) * 2));
   const int mleft = g.M - m0, nleft = g.N - n0;
-  const int nk = (g.K + BK - 1) / BK;
+  const int nk = (Keff + BK - 1) / BK;
 
   f32x4 acc[8][NTN];
 #pragma unroll
@@ -178,11 +159,23 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
 #pragma unroll
     for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 Aa[4], Ab[4], Ba[NTN], Bb[NTN];
+  // RoPE epilogue operands, fetched now so their latency hides under the main loop: the token id
+  // of tile row tid and entry tid of the cos/sin tables.
+  int pf_id = 0;
+  float pf_c = 0.f, pf_s = 0.f;
+  if constexpr (EPI == EPI_ROPE) {
+    const int t = threadIdx.x;
+    if (t < BM && m0 + t < g.M) pf_id = g.rope.ids ? g.rope.ids[m0 + t] : (m0 + t) % g.rope.mod;
+    if (t < g.rope.npos * g.rope.half) {
+      pf_c = g.rope.cos_t[t];
+      pf_s = g.rope.sin_t[t];
+    }
+  }
 
   auto load_tile = [&](int t) {
     LDS_AS char* s = smem + (t & 1) * STAGE;
-    stage<AK, BM>(ra, g.lda, mleft, t * BK, g.K, s, wave, lane);
-    stage<BKM, BN>(rb, g.ldb, nleft, t * BK, g.K, s + A_BYTES, wave, lane);
+    stage<AK, BM>(ra, g.lda, mleft, t * BK, Keff, s, wave, lane);
+    stage<BKM, BN>(rb, g.ldb, nleft, t * BK, Keff, s + A_BYTES, wave, lane);
   };
   // A fragments of M-half mh (4 m-tiles), k-step ks; B fragments of all NTN n-tiles, k-step ks
   auto rdA = [&](bf16x8 (&X)[4], int t, int mh, int ks) {
@@ -215,21 +208,38 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
   // fragments of the NEXT phase are read while the current phase's MFMAs run. One barrier per
   // tile, before phase 3 (whose prefetch reads tile t+1): it retires this wave's DMA of tile t+1
   // (issued one tile earlier) and its reads of tile t; then tile t+2 is DMA'd into slot t&1.
+  // MN-major operands are read with asm transposed reads (ds_read_tr16_async): each phase first
+  // waits for the fragments it consumes (read in the previous phase), then issues the next reads.
+  constexpr bool ASYNC = !AK || !BKM;
+  auto release = [&](bf16x8 (&X)[4], bf16x8 (&Y)[NTN]) {
+    if constexpr (ASYNC) {
+      lds_wait();
+      tie(X);
+      tie(Y);
+    }
+  };
   for (int t = 0; t < nk; ++t) {
+    release(Aa, Ba);
     rdA(Ab, t, 1, 0);
     __builtin_amdgcn_sched_barrier(0);
     mm(Aa, 0, Ba);
     __builtin_amdgcn_sched_barrier(0);
+    release(Ab, Ba);
     rdA(Aa, t, 0, 1);
     rdB(Bb, t, 1);
     __builtin_amdgcn_sched_barrier(0);
     mm(Ab, 1, Ba);
     __builtin_amdgcn_sched_barrier(0);
+    release(Aa, Bb);
     rdA(Ab, t, 1, 1);
     __builtin_amdgcn_sched_barrier(0);
     mm(Aa, 0, Bb);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if constexpr (ASYNC) {
+      tie(Ab);
+      tie(Bb);
+    }
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (t + 2 < nk) load_tile(t + 2);
@@ -244,8 +254,43 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
 
   // ---- epilogue: 4 passes of 2 m-tiles (32 rows) per wave through a padded LDS image
   constexpr int STR = WN + 4;  // floats per staged row (conflict-free ds_write_b32)
+  constexpr int LPR = WN / 4;  // lanes per staged row (16-B each)
+  constexpr int RPI = 64 / LPR;  // rows per wave-instruction
   __syncthreads();
   LDS_AS float* wl = (LDS_AS float*)(smem + wave * 32 * STR * 4);
+  // RoPE (modules.py:26-50, 343-365) on q/k columns: the tile rows' (frame, row, col) positions and
+  // the interleaved cos/sin table go to LDS behind the staging image; each thread's 4 columns fix
+  // its slice/axis/frequency once, so a store costs 1 + 4 LDS reads and 8 FMAs.
+  constexpr int ROPE_OFF = 8 * 32 * STR * 4;
+  LDS_AS int* rpos = (LDS_AS int*)(smem + ROPE_OFF);
+  LDS_AS f32x2* rtab = (LDS_AS f32x2*)(smem + ROPE_OFF + BM * 4);
+  bool ract[2] = {false, false};
+  int rsh[2] = {0, 0}, rf0[2] = {0, 0}, rf1[2] = {0, 0};
+  if constexpr (EPI == EPI_ROPE) {
+    const RopeP& r = g.rope;
+    const int t = threadIdx.x;
+    if (t < BM) {
+      const int fr = pf_id / r.tpf, rem = pf_id - r.tpf * fr, hr = rem / r.tpr;
+      rpos[t] = fr | (hr << 10) | ((rem - r.tpr * hr) << 20);
+    }
+    const int ntab = r.npos * r.half;
+    if (t < ntab) rtab[t] = f32x2{pf_c, pf_s};
+    for (int i = t + 512; i < ntab; i += 512) rtab[i] = f32x2{r.cos_t[i], r.sin_t[i]};
+    const int n = n0 + wc * WN + (lane % LPR) * 4, sw = 2 * r.half, e0 = (n % r.D) % r.hd;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int e = e0 + 2 * p, ax = e / sw, js = e - ax * sw;
+      ract[p] = n < 2 * r.D && e < 3 * sw;
+      rsh[p] = 10 * ax;
+      rf0[p] = js % r.half;
+      rf1[p] = (js + 1) % r.half;
+    }
+    __syncthreads();
+  }
+  const int col = (lane % LPR) * 4;  // this thread's 4 columns, fixed for every row it stores
+  const int ncol = n0 + wc * WN + col;
+  float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (EPI != EPI_GELU_BWD && EPI != EPI_PARTIAL && g.bias && ncol < g.N) bias4 = *(const float4*)(g.bias + ncol);
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
 #pragma unroll
@@ -256,28 +301,50 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
         for (int r = 0; r < 4; ++r)
           wl[(ii * 16 + (lane >> 4) * 4 + r) * STR + j * 16 + (lane & 15)] = acc[pass * 2 + ii][j][r];
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): own writes visible to own reads (wave-private)
-    constexpr int LPR = WN / 4;          // lanes per staged row (16-B each)
-    constexpr int RPI = 64 / LPR;        // rows per wave-instruction
+    // residual / GELU pre-activation rows of this pass fetched up front: one memory latency per
+    // pass instead of one per row
+    constexpr int IT = 32 / RPI;
+    [[maybe_unused]] float4 rres[EPI == EPI_F32_RESID ? IT : 1];
+    [[maybe_unused]] uint2 rpre[EPI == EPI_GELU_BWD ? IT : 1];
+    if constexpr (EPI == EPI_F32_RESID || EPI == EPI_GELU_BWD) {
 #pragma unroll
-    for (int it = 0; it < 32 / RPI; ++it) {
+      for (int it = 0; it < IT; ++it) {
+        const int m = m0 + wr * 128 + pass * 32 + it * RPI + lane / LPR;
+        const bool ok = m < g.M && ncol < g.N;
+        const long mm = ok ? m : 0;
+        const int nn = ok ? ncol : 0;
+        if constexpr (EPI == EPI_F32_RESID) rres[it] = *(const float4*)((const float*)g.aux + mm * g.ldaux + nn);
+        else rpre[it] = *(const uint2*)((const bf16_t*)g.aux + mm * g.ldaux + nn);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
       const int row = it * RPI + lane / LPR;
-      const int col = (lane % LPR) * 4;
       const f32x4 v4 = *(const LDS_AS f32x4*)(wl + row * STR + col);
       const int m = m0 + wr * 128 + pass * 32 + row;
-      const int n = n0 + wc * WN + col;
+      const int n = ncol;
       if (m >= g.M || n >= g.N) continue;
-      float v[4] = {v4[0], v4[1], v4[2], v4[3]};
-      if (EPI != EPI_GELU_BWD && g.bias) {
-        const float4 bb = *(const float4*)(g.bias + n);
-        v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
-      }
+      float v[4] = {v4[0] + bias4.x, v4[1] + bias4.y, v4[2] + bias4.z, v4[3] + bias4.w};
       if constexpr (EPI == EPI_BF16 || EPI == EPI_ROPE) {
-        if constexpr (EPI == EPI_ROPE) rope4(g.rope, m, n, v);
+        if constexpr (EPI == EPI_ROPE) {
+          const int rp = rpos[wr * 128 + pass * 32 + row];
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            if (!ract[p]) continue;
+            const int pos = min((rp >> rsh[p]) & 1023, g.rope.npos - 1) * g.rope.half;
+            const f32x2 a = rtab[pos + rf0[p]], b = rtab[pos + rf1[p]];
+            const float x0 = v[2 * p], x1 = v[2 * p + 1];
+            v[2 * p] = x0 * a[0] - x1 * a[1];
+            v[2 * p + 1] = x1 * b[0] + x0 * b[1];
+          }
+        }
         *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
       } else if constexpr (EPI == EPI_F32) {
         *(float4*)((float*)g.C + (long)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+      } else if constexpr (EPI == EPI_PARTIAL) {
+        *(float4*)(g.ws + ((long)blockIdx.y * g.M + m) * g.N + n) = make_float4(v[0], v[1], v[2], v[3]);
       } else if constexpr (EPI == EPI_F32_RESID) {
-        const float4 rr = *(const float4*)((const float*)g.aux + (long)m * g.ldaux + n);
+        const float4 rr = rres[it];
         *(float4*)((float*)g.C + (long)m * g.ldc + n) = make_float4(rr.x + v[0], rr.y + v[1], rr.z + v[2], rr.w + v[3]);
       } else if constexpr (EPI == EPI_GELU) {
         const uint32_t p0 = pack_bf2(v[0], v[1]), p1 = pack_bf2(v[2], v[3]);
@@ -286,7 +353,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
         *(uint2*)((bf16_t*)g.C2 + (long)m * g.ldc2 + n) =
             make_uint2(pack_bf2(gelu_fast(x0), gelu_fast(x1)), pack_bf2(gelu_fast(x2), gelu_fast(x3)));
       } else {  // EPI_GELU_BWD
-        const uint2 pu = *(const uint2*)((const bf16_t*)g.aux + (long)m * g.ldaux + n);
+        const uint2 pu = rpre[it];
         const float x0 = bf2f(pu.x & 0xffff), x1 = bf2f(pu.x >> 16), x2 = bf2f(pu.y & 0xffff), x3 = bf2f(pu.y >> 16);
         *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) =
             make_uint2(pack_bf2(v[0] * gelu_grad_fast(x0), v[1] * gelu_grad_fast(x1)),
@@ -298,8 +365,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
 }
 
 template <bool AK, bool BKM, int BN>
-int launch256(int epi, const G256& g, hipStream_t st) {
-  dim3 grid(g.tiles_m * g.tiles_n);
+int launch256(int epi, const G256& g, hipStream_t st, int splitk = 1) {
+  dim3 grid(g.tiles_m * g.tiles_n, splitk);
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_BF16, BN>), grid, dim3(512), 0, st, g); break;
     case EPI_F32: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_F32, BN>), grid, dim3(512), 0, st, g); break;
@@ -307,6 +374,13 @@ int launch256(int epi, const G256& g, hipStream_t st) {
     case EPI_GELU: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_GELU, BN>), grid, dim3(512), 0, st, g); break;
     case EPI_GELU_BWD: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_GELU_BWD, BN>), grid, dim3(512), 0, st, g); break;
     case EPI_ROPE: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_ROPE, BN>), grid, dim3(512), 0, st, g); break;
+    case EPI_PARTIAL:  // split-K weight gradients only: dY^T X, both operands MN-major
+      if constexpr (!AK && !BKM) {
+        hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_PARTIAL, BN>), grid, dim3(512), 0, st, g);
+        break;
+      } else {
+        return VJ_ERR_UNSUPPORTED;
+      }
     default: vj_set_error("gemm256: bad epilogue %d", epi); return VJ_ERR_ARG;
   }
   VJ_LAUNCH_CHECK("vj_gemm256");
@@ -325,11 +399,13 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
     return VJ_ERR_UNSUPPORTED;
   const int bn = (N % 256 == 0) ? 256 : 128;
   G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, C, ldc, C2, ldc2, bias, aux, ldaux,
-         vj_cdiv(M, 256), vj_cdiv(N, bn), RopeP{}};
+         vj_cdiv(M, 256), vj_cdiv(N, bn), RopeP{}, 0, nullptr};
   if (epi == EPI_ROPE) {
     if (!rope) return VJ_ERR_UNSUPPORTED;
     g.rope = *(const RopeP*)rope;
-    if (g.rope.hd % 4 || g.rope.D % 4) return VJ_ERR_UNSUPPORTED;
+    if (g.rope.hd % 4 || g.rope.D % 4 || g.rope.npos < 1 || g.rope.npos > 1024) return VJ_ERR_UNSUPPORTED;
+    const long lds_need = 8L * 32 * (bn / 4 + 4) * 4 + 256 * 4 + (long)g.rope.npos * g.rope.half * 8;
+    if (lds_need > 2L * (256 * BK * 2 + bn * BK * 2)) return VJ_ERR_UNSUPPORTED;
   }
   if (bn == 256) {
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
@@ -341,6 +417,19 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
   if (a_kmajor && !b_kmajor) return launch256<true, false, 128>(epi, g, st);
   if (!a_kmajor && b_kmajor) return launch256<false, true, 128>(epi, g, st);
   return launch256<false, false, 128>(epi, g, st);
+}
+
+// Split-K partial products ws[z] = A[:, z-th K slice] B[z-th K slice, :]^T (f32, [splitk][M][N]) with
+// 256-row tiles; the caller reduces the slabs. Returns VJ_ERR_UNSUPPORTED when it declines.
+int vj_gemm256_partial(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                       int b_kmajor, int kslice, int splitk, float* ws, hipStream_t st) {
+  if (a_kmajor || b_kmajor || N % 8 || M < 256 || N < 128) return VJ_ERR_UNSUPPORTED;
+  const int bn = (N % 256 == 0) ? 256 : 128;
+  G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
+         vj_cdiv(M, 256), vj_cdiv(N, bn), RopeP{}, kslice, ws};
+  if (splitk > 65535) return VJ_ERR_UNSUPPORTED;
+  return bn == 256 ? launch256<false, false, 256>(EPI_PARTIAL, g, st, splitk)
+                   : launch256<false, false, 128>(EPI_PARTIAL, g, st, splitk);
 }
 
 extern "C" int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
@@ -355,15 +444,15 @@ extern "C" int vj_rope(int T, int H, int hd, void* qkv, long ld, int q_off, int 
 // the 256-row kernel declines.
 extern "C" int vj_qkv_rope_gemm(int M, int K, const void* A, long lda, const void* B, long ldb, const float* bias,
                                 void* C, long ldc, int H, int hd, const int* ids, int ids_mod, int tpf, int tpr,
-                                const float* cos_t, const float* sin_t, void* stream) {
+                                const float* cos_t, const float* sin_t, int npos, void* stream) {
   if (M == 0) return VJ_OK;
   const int N = 3 * H * hd;
   VJ_CHECK_ARG(hd % 8 == 0 && cos_t && sin_t && (ids || ids_mod > 0), "vj_qkv_rope_gemm: bad rope arguments");
-  VJ_CHECK_ARG(tpf > 0 && tpr > 0, "vj_qkv_rope_gemm: tokens_per_frame/row must be > 0");
+  VJ_CHECK_ARG(tpf > 0 && tpr > 0 && npos > 0, "vj_qkv_rope_gemm: tokens_per_frame/row and npos must be > 0");
   const int half = (hd / 3) / 2;
   const char* e = getenv("VJ_GEMM256");
   if (M >= 1024 && !(e && e[0] == '0')) {
-    RopeP rp{ids, ids_mod, tpf, tpr, half, hd, H * hd, cos_t, sin_t};
+    RopeP rp{ids, ids_mod, tpf, tpr, half, hd, H * hd, cos_t, sin_t, npos};
     const int rc = vj_gemm256_dispatch(M, N, K, A, lda, 1, B, ldb, 1, EPI_ROPE, bias, nullptr, 0, C, ldc, nullptr, 0,
                                        (hipStream_t)stream, &rp);
     if (rc != VJ_ERR_UNSUPPORTED) return rc;

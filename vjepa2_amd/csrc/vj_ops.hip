@@ -194,20 +194,35 @@ __global__ __launch_bounds__(256) void k_colsum1(int M, int N, const void* __res
     if (n < N) ws[(long)blockIdx.y * N + n] = red[0][i] + red[1][i] + red[2][i] + red[3][i];
   }
 }
-// Stage 2: out[n] (+)= sum_s ws[s][n]; block = 64 columns x 4 row groups, fixed-order LDS combine.
-__global__ __launch_bounds__(256) void k_colsum2(int S, int N, const float* __restrict__ ws, long ws_ld,
-                                                 float* __restrict__ out, int acc) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int n = blockIdx.x * 64 + c;
-  float s = 0.f;
-  if (n < N)
-    for (int i = rg; i < S; i += 4) s += ws[(long)i * ws_ld + n];
-  red[rg][c] = s;
+// Stage 2: out[n] (+)= sum_s ws[s][n] (columns n >= split go to out2[n - split]). Block = 32
+// columns x 32 row groups; each thread keeps 4 independent partial sums so 8 loads are in flight,
+// then a fixed-order combine (deterministic, no atomics).
+__global__ __launch_bounds__(1024) void k_colsum2(int S, int N, const float* __restrict__ ws, long ws_ld,
+                                                  float* __restrict__ out, float* __restrict__ out2, int split,
+                                                  int acc) {
+  __shared__ float red[32][33];
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int n = blockIdx.x * 32 + c;
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    int i = rg;
+    for (; i + 7 * 32 < S; i += 8 * 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ws[(long)(i + u * 32) * ws_ld + n];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s4[u & 3] += v[u];
+    }
+    for (int u = 0; i < S; i += 32, ++u) s4[u & 3] += ws[(long)i * ws_ld + n];
+  }
+  red[rg][c] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   __syncthreads();
   if (rg == 0 && n < N) {
-    const float t = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
-    out[n] = acc ? out[n] + t : t;
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) t += red[r][c];
+    float* o = n < split ? out + n : out2 + (n - split);
+    *o = acc ? *o + t : t;
   }
 }
 
@@ -624,8 +639,12 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
   VJ_LAUNCH_CHECK("vj_layernorm_bwd");
   if (want_g) {
     // partials laid out [nb][2][D]: dgamma column sums over rows of stride 2D
-    if (dgamma) hipLaunchKernelGGL(k_colsum2, dim3((D + 63) / 64), dim3(256), 0, st, nb, D, ws, 2L * D, dgamma, 1);
-    if (dbeta) hipLaunchKernelGGL(k_colsum2, dim3((D + 63) / 64), dim3(256), 0, st, nb, D, ws + D, 2L * D, dbeta, 1);
+    if (dgamma && dbeta)
+      hipLaunchKernelGGL(k_colsum2, dim3((2 * D + 31) / 32), dim3(1024), 0, st, nb, 2 * D, ws, 2L * D, dgamma, dbeta, D, 1);
+    else if (dgamma)
+      hipLaunchKernelGGL(k_colsum2, dim3((D + 31) / 32), dim3(1024), 0, st, nb, D, ws, 2L * D, dgamma, nullptr, D, 1);
+    else
+      hipLaunchKernelGGL(k_colsum2, dim3((D + 31) / 32), dim3(1024), 0, st, nb, D, ws + D, 2L * D, dbeta, nullptr, D, 1);
     VJ_LAUNCH_CHECK("vj_layernorm_bwd(reduce)");
   }
   return VJ_OK;
@@ -644,7 +663,7 @@ extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, f
   dim3 g1((N + 511) / 512, S);
   if (x_bf16) hipLaunchKernelGGL(k_colsum1<true>, g1, dim3(256), 0, st, M, N, x, ld, rps, ws);
   else hipLaunchKernelGGL(k_colsum1<false>, g1, dim3(256), 0, st, M, N, x, ld, rps, ws);
-  hipLaunchKernelGGL(k_colsum2, dim3((N + 63) / 64), dim3(256), 0, st, S, N, ws, (long)N, out, accumulate);
+  hipLaunchKernelGGL(k_colsum2, dim3((N + 31) / 32), dim3(1024), 0, st, S, N, ws, (long)N, out, nullptr, N, accumulate);
   VJ_LAUNCH_CHECK("vj_colsum_f32");
   return VJ_OK;
 }

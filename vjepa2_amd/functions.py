@@ -40,19 +40,18 @@ def grad_buf(p):
 
 
 _ROPE_TABLES = {}
-ROPE_MAX_POS = 512
 
 
-def rope_tables(hd, device):
-    """cos/sin [512, half] of the reference's per-axis angles (modules.py:30-39, fp32 op order)."""
-    key = (hd, str(device))
+def rope_tables(hd, device, npos):
+    """cos/sin [npos, half] of the reference's per-axis angles (modules.py:30-39, fp32 op order)."""
+    key = (hd, str(device), npos)
     t = _ROPE_TABLES.get(key)
     if t is None:
         sw = 2 * ((hd // 3) // 2)
         omega = torch.arange(sw // 2, dtype=torch.float32)
         omega /= sw / 2.0
         omega = 1.0 / 10000**omega
-        freq = torch.arange(ROPE_MAX_POS, dtype=torch.float32)[:, None] * omega[None, :]
+        freq = torch.arange(npos, dtype=torch.float32)[:, None] * omega[None, :]
         t = (freq.cos().contiguous().to(device), freq.sin().contiguous().to(device))
         _ROPE_TABLES[key] = t
     return t
@@ -66,6 +65,8 @@ class TokenLayout:
         self.groups = [(int(n), int(l)) for n, l in groups if n > 0]
         self.T = sum(n * l for n, l in self.groups)
         self.ids, self.ids_mod, self.tpf, self.tpr = ids, int(ids_mod), int(tpf), int(tpr)
+        # positions per axis: frame < ceil(ids_mod / tpf), row < ceil(tpf / tpr), column < tpr
+        self.npos = max(-(-self.ids_mod // self.tpf), -(-self.tpf // self.tpr), self.tpr, 1)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -85,7 +86,7 @@ def block_forward(x, blk, lay, save):
     hd = D // H
     ln1, m1, r1 = ops.layernorm_fwd(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, want_stats=save)
     if attn.use_rope:  # QKV GEMM with RoPE of q, k fused into its epilogue
-        c, s = rope_tables(hd, x.device)
+        c, s = rope_tables(hd, x.device, lay.npos)
         qkv = ops.qkv_rope(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, H, hd, lay.ids, lay.ids_mod, lay.tpf,
                            lay.tpr, c, s)
     else:
@@ -135,7 +136,7 @@ def block_backward(dxo, blk, lay, saved):
     _bias_grad(attn.proj, dxm)
     rope = None
     if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
-        c, s = rope_tables(hd, x.device)
+        c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
     dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope)
     dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight))

@@ -116,10 +116,11 @@ class Block(nn.Module):
             tpf, tpr = g * g, g
         else:
             tpf, tpr = H_patches * W_patches, W_patches
-        ids = None
+        ids, nids = None, N
         if mask is not None:
             ids = ops.ids_to_int32([mask.to(device=device, dtype=torch.int64).contiguous()])
-        return fn.TokenLayout([(B, N)], ids=ids, ids_mod=N, tpf=tpf, tpr=tpr)
+            nids = int(mask.max()) + 1  # bounds the RoPE positions (table rows)
+        return fn.TokenLayout([(B, N)], ids=ids, ids_mod=nids, tpf=tpf, tpr=tpr)
 
     def forward(self, x, mask=None, attn_mask=None, T=None, H_patches=None, W_patches=None):
         if attn_mask is not None:

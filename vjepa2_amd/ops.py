@@ -98,10 +98,23 @@ def gemm(M, N, K, a, lda, a_kmajor, b, ldb, b_kmajor, epi, out=None, ldc=0, out2
 
 
 def wgrad_splitk(M, N, K, cus=256):
-    """Split K (tokens) until the grid has >= 2 tiles per CU, keeping >= 512 of K per slice."""
-    tiles = -(-M // 128) * -(-N // 128)
-    want = -(-2 * cus // tiles)
-    return max(1, min(want, K // 512))
+    """Split K (tokens) of a weight-gradient GEMM [M, N] += A[M, K] B[K, N]. Tiles are 256 x (256 or
+    128) when M >= 256 and N >= 128 (the C side's choice), else 128 x 128. Picks the split that
+    minimises (waves of tiles on the CUs) x (work per tile) + the f32 partial-slab traffic, keeping
+    >= 512 of K per slice."""
+    if M >= 256 and N >= 128:
+        tm, tn, per_cu = 256, (256 if N % 256 == 0 else 128), 1
+    else:
+        tm, tn, per_cu = 128, 128, 2
+    tiles = -(-M // tm) * -(-N // tn)
+    best, best_t = 1, None
+    for s in range(1, max(1, K // 512) + 1):
+        waves = -(-tiles * s // (cus * per_cu))
+        # ~1 PF/s over 256 CUs for the MFMA work, ~5 TB/s for writing + re-reading the slabs
+        t = waves * (K / s) * tm * tn * 2 / 3.9e12 + (s * M * N * 8 / 5.0e12 if s > 1 else 0.0)
+        if best_t is None or t < best_t * 0.98:
+            best, best_t = s, t
+    return best
 
 
 def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
@@ -242,7 +255,7 @@ def qkv_rope(x, w, bias, H, hd, ids, ids_mod, tpf, tpr, cos_tab, sin_tab):
     assert w.shape == (N, K) and x.dtype == BF16 and w.dtype == BF16
     out = torch.empty(M, N, dtype=BF16, device=x.device)
     _call("vj_qkv_rope_gemm", M, K, _p(x), _rowmajor(x, "x"), _p(w), _rowmajor(w, "w"), _p(bias), _p(out), N, H, hd,
-          _p(ids), int(ids_mod), int(tpf), int(tpr), _p(cos_tab), _p(sin_tab), _stream(),
+          _p(ids), int(ids_mod), int(tpf), int(tpr), _p(cos_tab), _p(sin_tab), cos_tab.shape[0], _stream(),
           label="k_gemm<1,1,EPI_ROPE>", flops=2.0 * M * N * K)
     return out
 

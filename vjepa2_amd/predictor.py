@@ -131,9 +131,9 @@ class VisionTransformerPredictor(nn.Module):
         if self.predictor_pos_embed is not None:
             pos = self.predictor_pos_embed[0].float().contiguous()
         if torch.is_grad_enabled() and (e.requires_grad or tok.requires_grad):
-            seq = fn._AssembleFn.apply(e, tok, pl.ctx_dst, pl.tgt_rows, pl.S, pos, pl.pos, self)
+            seq = fn._AssembleFn.apply(e, tok, pl.ctx_dst, pl.tgt_rows, pl.S, pos, pl.pos, self.mask_tokens)
         else:
-            seq = fn._AssembleFn.forward(_NoCtx(), e, tok, pl.ctx_dst, pl.tgt_rows, pl.S, pos, pl.pos, self)
+            seq = fn._AssembleFn.forward(_NoCtx(), e, tok, pl.ctx_dst, pl.tgt_rows, pl.S, pos, pl.pos, self.mask_tokens)
         g = self.grid_height
         lay = fn.TokenLayout(pl.groups, ids=pl.pos, ids_mod=self.num_patches, tpf=g * g, tpr=g)
         for blk in self.predictor_blocks:

@@ -1,0 +1,143 @@
+"""A/B timing of GEMM / attention kernel builds in ONE process (interleaved rounds, median).
+
+usage: python tools/bench_kernels.py [lib.so ...]   (default: vjepa2_amd/libvjepa_hip.so)
+Builds come from `python -m vjepa2_amd.build --variant NAME -DMACRO=...`. Random operands
+(uniform [-1, 1) scaled), shapes of the ViT-L/16 B=24 train step.
+"""
+import ctypes
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vjepa2_amd._lib import SIGNATURES  # noqa: E402
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    return lib
+
+
+# (name, M, N, K, a_kmajor, b_kmajor, epi, splitk)
+GEMMS = [
+    ("square4096", 4096, 4096, 4096, 1, 1, 1, 1),
+    ("qkv  ctx", 15424, 3072, 1024, 1, 1, 0, 1),
+    ("proj ctx", 15424, 1024, 1024, 1, 1, 2, 1),
+    ("fc1  ctx", 15424, 4096, 1024, 1, 1, 3, 1),
+    ("fc2  ctx", 15424, 1024, 4096, 1, 1, 2, 1),
+    ("fc1  tgt", 49152, 4096, 1024, 1, 1, 3, 1),
+    ("dgrad fc2", 15424, 4096, 1024, 1, 0, 0, 1),
+    ("dgrad fc1", 15424, 1024, 4096, 1, 0, 0, 1),
+    ("wgrad fc1", 4096, 1024, 15424, 0, 0, 2, 4),
+    ("wgrad qkv", 3072, 1024, 15424, 0, 0, 2, 5),
+    ("wgrad proj", 1024, 1024, 15424, 0, 0, 2, 15),
+    ("pred fc1", 98304, 1536, 384, 1, 1, 3, 1),
+    ("pred fc2", 98304, 384, 1536, 1, 1, 2, 1),
+]
+
+
+def gemm_case(lib, case, dev, stream):
+    name, M, N, K, akm, bkm, epi, sk = case
+    g = torch.Generator(device="cpu").manual_seed(0)
+    A = ((torch.rand(M, K, generator=g) * 2 - 1) if akm else (torch.rand(K, M, generator=g) * 2 - 1)).to(dev).bfloat16()
+    B = ((torch.rand(N, K, generator=g) * 2 - 1) if bkm else (torch.rand(K, N, generator=g) * 2 - 1)).to(dev).bfloat16()
+    lda = K if akm else M
+    ldb = K if bkm else N
+    bias = torch.zeros(N, device=dev)
+    if epi in (1, 2):
+        C = torch.zeros(M, N, device=dev)
+    else:
+        C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    C2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if epi == 3 else None
+    aux = C if epi == 2 else None
+    ws = torch.empty(max(1, sk * M * N if sk > 1 else 1), device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+
+    def run():
+        rc = lib.vj_gemm_bf16_splitk(M, N, K, p(A), lda, akm, p(B), ldb, bkm, epi, p(bias), p(aux), N if aux is not None else 0,
+                                     p(C) if epi != 3 else None, N if epi != 3 else 0, p(C2), N if C2 is not None else 0,
+                                     sk, p(ws), ws.numel(), stream)
+        assert rc == 0, rc
+    return run, 2.0 * M * N * K
+
+
+def attn_case(lib, hd, H, groups, dev, stream, bwd):
+    T = sum(n * l for n, l in groups)
+    D = H * hd
+    qkv = (torch.randn(T, 3 * D, device=dev)).bfloat16()
+    o = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+    stats = torch.empty(2, H, T, device=dev)
+    do = torch.randn(T, D, device=dev).bfloat16()
+    dqkv = torch.empty(T, 3 * D, device=dev, dtype=torch.bfloat16)
+    ns = (ctypes.c_int * len(groups))(*[g[0] for g in groups])
+    ln = (ctypes.c_int * len(groups))(*[g[1] for g in groups])
+    sc = hd ** -0.5
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def fwd():
+        assert lib.vj_attn_fwd(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(stats), sc, len(groups), ns, ln, stream) == 0
+    fwd()
+
+    def bwdf():
+        assert lib.vj_attn_bwd(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(do), D, P(stats), P(dqkv), 3 * D, sc,
+                               len(groups), ns, ln, None, 0, 0, 0, None, None, stream) == 0
+    fl = sum(4.0 * n * l * l * D for n, l in groups)
+    return (bwdf, 2 * fl) if bwd else (fwd, fl)
+
+
+def time_fn(fn, iters=10):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    paths = [a for a in sys.argv[1:] if a.endswith(".so")] or [os.path.join(HERE, "vjepa2_amd", "libvjepa_hip.so")]
+    rounds = 5
+    dev = torch.device("cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    libs = [load(pth) for pth in paths]
+    cases = []
+    only = os.environ.get("VJ_BENCH_ONLY", "")
+    for c in GEMMS:
+        if only and only not in c[0]:
+            continue
+        cases.append((c[0], [gemm_case(lib, c, dev, stream) for lib in libs]))
+    attn = [("attn fwd hd64 ctx", 64, 16, [(24, 513), (24, 130)], False),
+            ("attn fwd hd64 tgt", 64, 16, [(24, 2048)], False),
+            ("attn bwd hd64 ctx", 64, 16, [(24, 513), (24, 130)], True),
+            ("attn fwd hd32 pred", 32, 12, [(24, 2048), (24, 2048)], False),
+            ("attn bwd hd32 pred", 32, 12, [(24, 2048), (24, 2048)], True)]
+    for name, hd, H, groups, bwd in attn:
+        if only and only not in name:
+            continue
+        cases.append((name, [attn_case(lib, hd, H, groups, dev, stream, bwd) for lib in libs]))
+    print(f"{'case':22s} " + " ".join(f"{os.path.basename(pth)[:24]:>26s}" for pth in paths), flush=True)
+    for name, runs in cases:
+        res = [[] for _ in libs]
+        for _ in range(rounds):
+            for i, (fn, fl) in enumerate(runs):
+                res[i].append(time_fn(fn))
+        cols = []
+        for i, (fn, fl) in enumerate(runs):
+            ms = statistics.median(res[i])
+            cols.append(f"{ms * 1e3:9.1f}us {fl / ms / 1e9:7.1f}TF")
+        print(f"{name:22s} " + " ".join(f"{c:>26s}" for c in cols), flush=True)
+
+
+if __name__ == "__main__":
+    main()

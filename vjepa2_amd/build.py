@@ -37,15 +37,20 @@ def _needs_build(obj, src):
     return not os.path.exists(obj) or any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 
-def build(verbose=True, force=False):
-    objdir = os.path.join(HERE, "build")
+def build(verbose=True, force=False, variant=None, defines=()):
+    """Compile every source for gfx950 and link libvjepa_hip.so. `variant` builds an experimental
+    copy (libvjepa_hip_<variant>.so, objects in build/<variant>/) with extra -D `defines`, for
+    A/B timing of kernel variants inside one process (tools/bench_kernels.py)."""
+    objdir = os.path.join(HERE, "build", variant) if variant else os.path.join(HERE, "build")
+    lib = os.path.join(HERE, f"libvjepa_hip_{variant}.so") if variant else LIB
+    flags = CFLAGS + [f"-D{d}" for d in defines]
     os.makedirs(objdir, exist_ok=True)
     jobs = []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
-        if force or _needs_build(obj, src):
-            jobs.append([HIPCC, *CFLAGS, "-c", src, "-o", obj])
+        if force or variant or _needs_build(obj, src):
+            jobs.append([HIPCC, *flags, "-c", src, "-o", obj])
 
     def run(cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -58,16 +63,21 @@ def build(verbose=True, force=False):
             if verbose:
                 print(f"[vjepa2_amd.build] compiled {os.path.basename(o)}", file=sys.stderr)
     objs = [os.path.join(objdir, s.replace(".hip", ".o")) for s in SOURCES]
-    if force or jobs or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+    if force or jobs or not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs):
+        link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib, *objs]
         tl = _torch_libdir()
         if tl:
             link += [f"-L{tl}", f"-Wl,-rpath,{tl}"]
         run(link)
         if verbose:
-            print(f"[vjepa2_amd.build] linked {LIB}", file=sys.stderr)
-    return LIB
+            print(f"[vjepa2_amd.build] linked {lib}", file=sys.stderr)
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    args = sys.argv[1:]
+    var = None
+    if "--variant" in args:
+        var = args[args.index("--variant") + 1]
+    defs = [a[2:] for a in args if a.startswith("-D")]
+    build(force="--force" in args, variant=var, defines=defs)

@@ -189,11 +189,17 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
     for (int j = 0; j < NTN; ++j) Y[j] = frag<BKM, BN>(s, wc * WN + j * 16, ks, lane);
   };
   auto mm = [&](const bf16x8 (&X)[4], int mh, const bf16x8 (&Y)[NTN]) {
+#if VJ_GEMM_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < NTN; ++j)
         acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * 4 + i][j], 0, 0, 0);
+#if VJ_GEMM_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
   };
 
   // prologue: tiles 0 and 1 in flight, then the first fragments (phase 0 of tile 0)

@@ -85,12 +85,15 @@ def test_gemm_splitk(epi, MNK):
     assert torch.equal(out, first), "split-K must be deterministic"
 
 
+@pytest.mark.parametrize("N", [256, 384, 200])
 @pytest.mark.parametrize("M", [333, 1333])
-def test_gemm_epilogues(M):
+def test_gemm_epilogues(M, N):
+    """Every epilogue; M >= 1024 runs the 256-row kernel (N = 256: 256-wide tiles, 384 / 200: 128-wide,
+    200 ragged), whose K-major-B forms store straight from registers (permuted B staging)."""
     from vjepa2_amd import ops
 
     g = torch.Generator(device="cpu").manual_seed(0)
-    N, K = 256, 192
+    K = 192
     X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
     W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
     b = torch.randn(N, generator=g).to(DEV)
@@ -111,6 +114,14 @@ def test_gemm_epilogues(M):
     torch.nn.functional.gelu(x).backward(dY.float() @ W2.float())
     got = ops.linear_dgrad(dY, W2, gelu_pre=pre2)
     _close(got, x.grad, 2e-3, 1e-2, "EPI_GELU_BWD")
+    # the same with B K-major (direct-store epilogue) and the plain f32 epilogue
+    W2t = W2.t().contiguous()  # [K, N]: B(n=k_out, k=n_in) K-major
+    got2 = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(M, K, N, dY, N, True, W2t, N, True, ops.EPI_GELU_BWD, out=got2, ldc=K, aux=pre2, ldaux=K)
+    _close(got2, x.grad, 2e-3, 1e-2, "EPI_GELU_BWD (B K-major)")
+    f32 = torch.empty(M, K, device=DEV)
+    ops.gemm(M, K, N, dY, N, True, W2t, N, True, ops.EPI_F32, out=f32, ldc=K)
+    _close(f32, dY.float() @ W2.float(), 2e-4 * math.sqrt(N), 1e-5, "EPI_F32 (B K-major)")
     # wgrad accumulate
     dw = torch.randn(N, K, generator=g).to(DEV)
     exp = dw + dY.float().t() @ pre2.float()

@@ -29,18 +29,21 @@ def load(path):
 # (name, M, N, K, a_kmajor, b_kmajor, epi, splitk)
 GEMMS = [
     ("square4096", 4096, 4096, 4096, 1, 1, 1, 1),
-    ("qkv  ctx", 15424, 3072, 1024, 1, 1, 0, 1),
-    ("proj ctx", 15424, 1024, 1024, 1, 1, 2, 1),
-    ("fc1  ctx", 15424, 4096, 1024, 1, 1, 3, 1),
-    ("fc2  ctx", 15424, 1024, 4096, 1, 1, 2, 1),
+    ("qkv  ctx", 11712, 3072, 1024, 1, 1, 0, 1),
+    ("proj ctx", 11712, 1024, 1024, 1, 1, 2, 1),
+    ("fc1  ctx", 11712, 4096, 1024, 1, 1, 3, 1),
+    ("fc2  ctx", 11712, 1024, 4096, 1, 1, 2, 1),
     ("fc1  tgt", 49152, 4096, 1024, 1, 1, 3, 1),
-    ("dgrad fc2", 15424, 4096, 1024, 1, 0, 0, 1),
-    ("dgrad fc1", 15424, 1024, 4096, 1, 0, 0, 1),
-    ("wgrad fc1", 4096, 1024, 15424, 0, 0, 2, 4),
-    ("wgrad qkv", 3072, 1024, 15424, 0, 0, 2, 5),
-    ("wgrad proj", 1024, 1024, 15424, 0, 0, 2, 15),
-    ("pred fc1", 98304, 1536, 384, 1, 1, 3, 1),
-    ("pred fc2", 98304, 384, 1536, 1, 1, 2, 1),
+    ("dgrad fc2", 11712, 4096, 1024, 1, 0, 0, 1),
+    ("dgrad fc1", 11712, 1024, 4096, 1, 0, 0, 1),
+    ("wgrad fc1", 4096, 1024, 11712, 0, 0, 2, 4),
+    ("wgrad qkv", 3072, 1024, 11712, 0, 0, 2, 5),
+    ("wgrad proj", 1024, 1024, 11712, 0, 0, 2, 15),
+    ("pred qkv", 71232, 1152, 384, 1, 1, 0, 1),
+    ("pred dgrad fc1", 71232, 384, 1536, 1, 0, 0, 1),
+    ("pred wgrad fc1", 1536, 384, 71232, 0, 0, 2, 14),
+    ("pred fc1", 71232, 1536, 384, 1, 1, 3, 1),
+    ("pred fc2", 71232, 384, 1536, 1, 1, 2, 1),
 ]
 
 
@@ -117,11 +120,11 @@ def main():
         if only and only not in c[0]:
             continue
         cases.append((c[0], [gemm_case(lib, c, dev, stream) for lib in libs]))
-    attn = [("attn fwd hd64 ctx", 64, 16, [(24, 513), (24, 130)], False),
+    attn = [("attn fwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], False),
             ("attn fwd hd64 tgt", 64, 16, [(24, 2048)], False),
-            ("attn bwd hd64 ctx", 64, 16, [(24, 513), (24, 130)], True),
-            ("attn fwd hd32 pred", 32, 12, [(24, 2048), (24, 2048)], False),
-            ("attn bwd hd32 pred", 32, 12, [(24, 2048), (24, 2048)], True)]
+            ("attn bwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], True),
+            ("attn fwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], False),
+            ("attn bwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], True)]
     for name, hd, H, groups, bwd in attn:
         if only and only not in name:
             continue

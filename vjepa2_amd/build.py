@@ -46,8 +46,9 @@ def build(verbose=True, force=False, variant=None, defines=()):
     flags = CFLAGS + [f"-D{d}" for d in defines]
     os.makedirs(objdir, exist_ok=True)
     jobs = []
+    csrc = os.environ.get("VJ_CSRC", CSRC) if variant else CSRC  # variant may build another source tree
     for s in SOURCES:
-        src = os.path.join(CSRC, s)
+        src = os.path.join(csrc, s)
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
         if force or variant or _needs_build(obj, src):
             jobs.append([HIPCC, *flags, "-c", src, "-o", obj])

@@ -294,7 +294,10 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
   dim3 grid(vj_cdiv(N, BN), vj_cdiv(M, BM), splitk);
   VJ_CHECK_ARG(grid.y <= 65535, "vj_gemm_bf16: M too large");
   hipStream_t st = (hipStream_t)stream;
-  if (splitk == 1 && M >= 1024 && N >= 128 && use_gemm256()) {
+#ifndef VJ_GEMM256_MINK
+#define VJ_GEMM256_MINK 0
+#endif
+  if (splitk == 1 && M >= 1024 && N >= 128 && K >= VJ_GEMM256_MINK && use_gemm256()) {
     const int rc = vj_gemm256_dispatch(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, epi, bias, aux, ldaux, C, ldc, C2,
                                        ldc2, st, nullptr);
     if (rc != VJ_ERR_UNSUPPORTED) return rc;

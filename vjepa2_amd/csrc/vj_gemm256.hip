@@ -56,7 +56,10 @@ __device__ __forceinline__ int mn_swz(int k) { return 2 * (k & 3) + 8 * ((k >> 3
 
 // K-major image: [ROWS][64] bf16, 128-B rows, chunk ^= (row>>1)&7.
 // MN-major image: [64][ROWS] bf16, ROWS*2-B rows, chunk ^= mn_swz(k).
-template <bool KMAJ, int ROWS>
+// PERM (K-major B only): LDS row r of each WN-row group holds global row NTN*(r%16) + r/16 of the
+// group, so n-tile j of the MFMA accumulators covers the group's columns {NTN*c + j}: each lane
+// then owns NTN CONSECUTIVE output columns and the epilogue stores straight from registers.
+template <bool KMAJ, int ROWS, bool PERM = false>
 __device__ __forceinline__ void stage(__amdgpu_buffer_rsrc_t rs, long ld, int rows_left, int k0, int K,
                                       LDS_AS char* lds, int wave, int lane) {
   constexpr int PIECES = ROWS / 8;  // 1-KB DMA pieces per operand tile
@@ -68,7 +71,13 @@ __device__ __forceinline__ void stage(__amdgpu_buffer_rsrc_t rs, long ld, int ro
       const int r = p * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((r >> 1) & 7);
       const int kk = k0 + c * 8;
-      voff = (r < rows_left && kk < K) ? (uint32_t)(((long)r * ld + kk) * 2) : VJ_OOB;
+      int gr = r;
+      if constexpr (PERM) {
+        constexpr int WN = ROWS / 4, NTN = WN / 16;
+        const int rl = r % WN;
+        gr = (r - rl) + NTN * (rl & 15) + (rl >> 4);
+      }
+      voff = (gr < rows_left && kk < K) ? (uint32_t)(((long)gr * ld + kk) * 2) : VJ_OOB;
     } else {
       constexpr int CPR = ROWS / 8;     // chunks per LDS row
       constexpr int RPP = 64 / CPR;     // k-rows per piece
@@ -127,6 +136,9 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
   constexpr int WN = BN / 4;      // wave tile columns (64 / 32)
   constexpr int NTN = WN / 16;    // 16-wide n tiles per wave (4 / 2)
   constexpr int NH = NTN / 2;     // n tiles per N-half register set
+  // K-major B with 4 n-tiles per wave: permuted B staging + stores straight from registers (16-B
+  // f32 / 8-B bf16 per row); 128-wide tiles would store 4-8 B per lane, so they keep the LDS path
+  constexpr bool DIRECT = BKM && NTN == 4;
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
 
@@ -175,7 +187,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
   auto load_tile = [&](int t) {
     LDS_AS char* s = smem + (t & 1) * STAGE;
     stage<AK, BM>(ra, g.lda, mleft, t * BK, Keff, s, wave, lane);
-    stage<BKM, BN>(rb, g.ldb, nleft, t * BK, Keff, s + A_BYTES, wave, lane);
+    stage<BKM, BN, DIRECT>(rb, g.ldb, nleft, t * BK, Keff, s + A_BYTES, wave, lane);
   };
   // A fragments of M-half mh (4 m-tiles), k-step ks; B fragments of all NTN n-tiles, k-step ks
   auto rdA = [&](bf16x8 (&X)[4], int t, int mh, int ks) {
@@ -258,6 +270,139 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
     __builtin_amdgcn_sched_barrier(0);
   }
 
+  if constexpr (DIRECT) {
+    // ---- direct epilogue (K-major B staged with PERM): lane (c = lane&15, g = lane>>4) owns rows
+    // i*16 + 4g + r of m-tile i and the NTN consecutive columns nb .. nb+NTN-1, so every row goes
+    // out of registers as one 8/16-B store; no LDS round trip.
+    const int nb = n0 + wc * WN + NTN * (lane & 15);
+    const bool nok = nb < g.N;
+    const int mb = m0 + wr * 128 + 4 * (lane >> 4);
+    float bias[NTN];
+#pragma unroll
+    for (int j = 0; j < NTN; ++j) bias[j] = 0.f;
+    if (EPI != EPI_GELU_BWD && EPI != EPI_PARTIAL && g.bias && nok)
+#pragma unroll
+      for (int j = 0; j < NTN; ++j) bias[j] = g.bias[nb + j];
+    // RoPE (modules.py:26-50, 343-365): tile rows' (frame, row, col) positions + interleaved
+    // cos/sin table in LDS; this lane's NTN/2 column pairs fix slice/axis/frequency once.
+    [[maybe_unused]] LDS_AS int* rpos = (LDS_AS int*)smem;
+    [[maybe_unused]] LDS_AS f32x2* rtab = (LDS_AS f32x2*)(smem + BM * 4);
+    [[maybe_unused]] bool ract[NTN / 2];
+    [[maybe_unused]] int rsh[NTN / 2], rf0[NTN / 2], rf1[NTN / 2];
+    if constexpr (EPI == EPI_ROPE) {
+      __syncthreads();  // every wave is done with the operand stages
+      const RopeP& r = g.rope;
+      const int t = threadIdx.x;
+      if (t < BM) {
+        const int fr = pf_id / r.tpf, rem = pf_id - r.tpf * fr, hr = rem / r.tpr;
+        rpos[t] = fr | (hr << 10) | ((rem - r.tpr * hr) << 20);
+      }
+      const int ntab = r.npos * r.half;
+      if (t < ntab) rtab[t] = f32x2{pf_c, pf_s};
+      for (int i = t + 512; i < ntab; i += 512) rtab[i] = f32x2{r.cos_t[i], r.sin_t[i]};
+      const int sw = 2 * r.half, e0 = (nb % r.D) % r.hd;
+#pragma unroll
+      for (int p = 0; p < NTN / 2; ++p) {
+        const int e = e0 + 2 * p, ax = e / sw, js = e - ax * sw;
+        ract[p] = nok && nb < 2 * r.D && e < 3 * sw;
+        rsh[p] = 10 * ax;
+        rf0[p] = js % r.half;
+        rf1[p] = (js + 1) % r.half;
+      }
+      __syncthreads();
+    }
+    // residual (f32) / pre-activation (bf16) rows: m-tile i+1's fetched while m-tile i is stored
+    constexpr bool AUX = EPI == EPI_F32_RESID || EPI == EPI_GELU_BWD;
+    [[maybe_unused]] float aux[2][4][NTN];
+    auto fetch = [&](int i, float (&dst)[4][NTN]) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mb + i * 16 + r;
+        const bool ok = m < g.M && nok;
+        const long off = ok ? (long)m * g.ldaux + nb : 0;
+        if constexpr (EPI == EPI_F32_RESID) {
+          if constexpr (NTN == 4) {
+            const float4 x = *(const float4*)((const float*)g.aux + off);
+            dst[r][0] = x.x; dst[r][1] = x.y; dst[r][2] = x.z; dst[r][3] = x.w;
+          } else {
+            const float2 x = *(const float2*)((const float*)g.aux + off);
+            dst[r][0] = x.x; dst[r][1] = x.y;
+          }
+        } else {
+          if constexpr (NTN == 4) {
+            const uint2 x = *(const uint2*)((const bf16_t*)g.aux + off);
+            dst[r][0] = bf2f(x.x & 0xffff); dst[r][1] = bf2f(x.x >> 16);
+            dst[r][2] = bf2f(x.y & 0xffff); dst[r][3] = bf2f(x.y >> 16);
+          } else {
+            const uint32_t x = *(const uint32_t*)((const bf16_t*)g.aux + off);
+            dst[r][0] = bf2f(x & 0xffff); dst[r][1] = bf2f(x >> 16);
+          }
+        }
+      }
+    };
+    if constexpr (AUX) fetch(0, aux[0]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr (AUX) {
+        if (i + 1 < 8) fetch(i + 1, aux[(i + 1) & 1]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mb + i * 16 + r;
+        if (m >= g.M || !nok) continue;
+        float v[NTN];
+#pragma unroll
+        for (int j = 0; j < NTN; ++j) v[j] = acc[i][j][r] + bias[j];
+        if constexpr (EPI == EPI_ROPE) {
+          const int rp = rpos[wr * 128 + i * 16 + 4 * (lane >> 4) + r];
+#pragma unroll
+          for (int p = 0; p < NTN / 2; ++p) {
+            if (!ract[p]) continue;
+            const int pos = min((rp >> rsh[p]) & 1023, g.rope.npos - 1) * g.rope.half;
+            const f32x2 a = rtab[pos + rf0[p]], b = rtab[pos + rf1[p]];
+            const float x0 = v[2 * p], x1 = v[2 * p + 1];
+            v[2 * p] = x0 * a[0] - x1 * a[1];
+            v[2 * p + 1] = x1 * b[0] + x0 * b[1];
+          }
+        }
+        if constexpr (EPI == EPI_F32_RESID) {
+#pragma unroll
+          for (int j = 0; j < NTN; ++j) v[j] += aux[i & 1][r][j];
+        }
+        if constexpr (EPI == EPI_F32 || EPI == EPI_F32_RESID || EPI == EPI_PARTIAL) {
+          float* dst = EPI == EPI_PARTIAL ? g.ws + ((long)blockIdx.y * g.M + m) * g.N + nb
+                                          : (float*)g.C + (long)m * g.ldc + nb;
+          if constexpr (NTN == 4) *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
+          else *(float2*)dst = make_float2(v[0], v[1]);
+        } else {
+          uint32_t pk[NTN / 2];
+#pragma unroll
+          for (int q = 0; q < NTN / 2; ++q) {
+            if constexpr (EPI == EPI_GELU_BWD)
+              pk[q] = pack_bf2(v[2 * q] * gelu_grad_fast(aux[i & 1][r][2 * q]),
+                               v[2 * q + 1] * gelu_grad_fast(aux[i & 1][r][2 * q + 1]));
+            else
+              pk[q] = pack_bf2(v[2 * q], v[2 * q + 1]);
+          }
+          if (EPI != EPI_GELU || g.C) {
+            bf16_t* dst = (bf16_t*)g.C + (long)m * g.ldc + nb;
+            if constexpr (NTN == 4) *(uint2*)dst = make_uint2(pk[0], pk[1]);
+            else *(uint32_t*)dst = pk[0];
+          }
+          if constexpr (EPI == EPI_GELU) {
+            uint32_t ga[NTN / 2];
+#pragma unroll
+            for (int q = 0; q < NTN / 2; ++q)
+              ga[q] = pack_bf2(gelu_fast(bf2f(pk[q] & 0xffff)), gelu_fast(bf2f(pk[q] >> 16)));
+            bf16_t* dst2 = (bf16_t*)g.C2 + (long)m * g.ldc2 + nb;
+            if constexpr (NTN == 4) *(uint2*)dst2 = make_uint2(ga[0], ga[1]);
+            else *(uint32_t*)dst2 = ga[0];
+          }
+        }
+      }
+    }
+    return;
+  }
   // ---- epilogue: 4 passes of 2 m-tiles (32 rows) per wave through a padded LDS image
   constexpr int STR = WN + 4;  // floats per staged row (conflict-free ds_write_b32)
   constexpr int LPR = WN / 4;  // lanes per staged row (16-B each)

@@ -79,11 +79,14 @@ int vj_qkv_rope_gemm(int M, int K, const void* A, long lda, const void* B, long 
 int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma, const float* beta,
                      float eps, void* y, int y_f32, long ldy, float* mean, float* rstd, void* stream);
 /* Backward (dy bf16): dres(f32) = (dres_in or 0) + dx; optional bf16 copy of dres; dgamma/dbeta
- * accumulated (+=) through a workspace of vj_layernorm_bwd_blocks(M)*2*D floats. */
+ * accumulated (+=) through a workspace of vj_layernorm_bwd_blocks(M)*2*D floats. Optional sum_in / sum_out
+ * (+=) column sums of dres_in / dres (the fc2 / proj bias gradients, modules.py:77-83, 326-382); with
+ * either, the workspace needs vj_layernorm_bwd_blocks(M)*4*D floats. */
 int vj_layernorm_bwd_blocks(int M);
 int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const float* x, long ldx, const float* mean,
                      const float* rstd, const float* gamma, const float* dres_in, long ldri, float* dres, long ldr,
-                     void* dres_bf16, long ldrb, float* dgamma, float* dbeta, float* ws, long ws_floats, void* stream);
+                     void* dres_bf16, long ldrb, float* dgamma, float* dbeta, float* sum_in, float* sum_out, float* ws,
+                     long ws_floats, void* stream);
 
 /* out[n] (+)= sum_m x[m, n]  (bias gradients), N % 8 == 0. ws >= min(256, ceil(M/64)) * N floats. */
 int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate, float* ws,

@@ -106,6 +106,9 @@ def test_gemm_epilogues(M, N):
     pre, act = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
     _close(pre, ref, 1e-3, 8e-3, "EPI_GELU pre")
     _close(act, torch.nn.functional.gelu(pre.float()), 1e-3, 8e-3, "EPI_GELU act")
+    if M >= 1024:  # GELU of the bf16 pre-activation, rounded once (erf polynomial, |err| <= 1.5e-7)
+        exact = act == torch.nn.functional.gelu(pre.float()).bfloat16()
+        assert float(exact.float().mean()) > 0.995  # erf polynomial: 1-ulp ties at rounding boundaries
     # GELU backward epilogue: out = (dY W) * gelu'(pre)
     dY = torch.randn(M, N, generator=g).to(DEV).bfloat16()
     W2 = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
@@ -200,6 +203,15 @@ def test_layernorm(D):
     _close(dres_bf, xr.grad + dres_in, 1e-3, 8e-3, "ln bwd dx bf16")
     _close(dw, wr.grad, 1e-3, 1e-4, "ln bwd dgamma")
     _close(db, br.grad, 1e-3, 1e-4, "ln bwd dbeta")
+    # fused bias gradients: column sums of dres_in and of dres, accumulated
+    dw2, db2 = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    s_in, s_out = torch.ones(D, device=DEV), torch.ones(D, device=DEV)
+    dres2, _ = ops.layernorm_bwd(dy, x, mean, rstd, w, dres_in=dres_in, dweight=dw2, dbias=db2, sum_in=s_in,
+                                 sum_out=s_out)
+    torch.cuda.synchronize()
+    assert torch.equal(dres2, dres) and torch.equal(dw2, dw) and torch.equal(db2, db)
+    _close(s_in, 1 + dres_in.sum(0), 1e-3, 1e-4, "ln bwd sum(dres_in)")
+    _close(s_out, 1 + (xr.grad + dres_in).sum(0), 1e-3, 1e-4, "ln bwd sum(dres)")
 
 
 def test_colsum():

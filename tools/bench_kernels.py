@@ -36,6 +36,8 @@ GEMMS = [
     ("fc1  tgt", 49152, 4096, 1024, 1, 1, 3, 1),
     ("dgrad fc2", 11712, 4096, 1024, 1, 0, 0, 1),
     ("dgrad fc1", 11712, 1024, 4096, 1, 0, 0, 1),
+    ("dgrad fc2 GELU_BWD", 11712, 4096, 1024, 1, 0, 4, 1),
+    ("pred dgrad fc2 GELU_BWD", 71232, 1536, 384, 1, 0, 4, 1),
     ("wgrad fc1", 4096, 1024, 11712, 0, 0, 2, 4),
     ("wgrad qkv", 3072, 1024, 11712, 0, 0, 2, 5),
     ("wgrad proj", 1024, 1024, 11712, 0, 0, 2, 15),
@@ -60,7 +62,7 @@ def gemm_case(lib, case, dev, stream):
     else:
         C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     C2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if epi == 3 else None
-    aux = C if epi == 2 else None
+    aux = C if epi == 2 else ((torch.rand(M, N, generator=g) * 4 - 2).to(dev).bfloat16() if epi == 4 else None)
     ws = torch.empty(max(1, sk * M * N if sk > 1 else 1), device=dev)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
 
@@ -110,7 +112,7 @@ def time_fn(fn, iters=10):
 
 def main():
     paths = [a for a in sys.argv[1:] if a.endswith(".so")] or [os.path.join(HERE, "vjepa2_amd", "libvjepa_hip.so")]
-    rounds = 5
+    rounds = int(os.environ.get("VJ_BENCH_ROUNDS", "7"))
     dev = torch.device("cuda")
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     libs = [load(pth) for pth in paths]

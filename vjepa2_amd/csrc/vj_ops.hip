@@ -83,12 +83,17 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
                                                 const float* __restrict__ x, long ldx, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                 const float* __restrict__ dres_in, long ldri, float* __restrict__ dres,
-                                                long ldr, bf16_t* __restrict__ dres_bf, long ldrb, float* __restrict__ ws) {
-  __shared__ float red[2][NV * 256];  // D <= 2048
+                                                long ldr, bf16_t* __restrict__ dres_bf, long ldrb, float* __restrict__ ws,
+                                                int nsum) {
+  // column partials per block, [nsum][D]: dgamma, dbeta, then (nsum == 4) sum of dres_in and of dres
+  // (the bias gradients of the Linear layers whose outputs these are: fc2 and proj, modules.py:77-83)
+  __shared__ float red[4][NV * 256];  // D <= 2048
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float4 dg[NV], db[NV];
+  float4 acc[4][NV];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) dg[i] = db[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) acc[k][i] = make_float4(0.f, 0.f, 0.f, 0.f);
   for (long row = (long)blockIdx.x * 4 + wave; row < M; row += (long)gridDim.x * 4) {
     const float mu = mean[row], rs = rstd[row];
     float4 xh[NV], g[NV];
@@ -101,8 +106,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
         const uint2 u = *(const uint2*)(dy + row * lddy + c);
         const float4 d = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
         xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
-        db[i].x += d.x; db[i].y += d.y; db[i].z += d.z; db[i].w += d.w;
-        dg[i].x += d.x * xh[i].x; dg[i].y += d.y * xh[i].y; dg[i].z += d.z * xh[i].z; dg[i].w += d.w * xh[i].w;
+        acc[1][i].x += d.x; acc[1][i].y += d.y; acc[1][i].z += d.z; acc[1][i].w += d.w;
+        acc[0][i].x += d.x * xh[i].x; acc[0][i].y += d.y * xh[i].y;
+        acc[0][i].z += d.z * xh[i].z; acc[0][i].w += d.w * xh[i].w;
         float4 gm = make_float4(1.f, 1.f, 1.f, 1.f);
         if (gamma) gm = *(const float4*)(gamma + c);
         g[i] = make_float4(d.x * gm.x, d.y * gm.y, d.z * gm.z, d.w * gm.w);
@@ -119,8 +125,10 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
                                 rs * (g[i].z - m1 - xh[i].z * m2), rs * (g[i].w - m1 - xh[i].w * m2));
         if constexpr (ACC) {
           const float4 o = *(const float4*)(dres_in + row * ldri + c);
+          acc[2][i].x += o.x; acc[2][i].y += o.y; acc[2][i].z += o.z; acc[2][i].w += o.w;
           dx.x += o.x; dx.y += o.y; dx.z += o.z; dx.w += o.w;
         }
+        acc[3][i].x += dx.x; acc[3][i].y += dx.y; acc[3][i].z += dx.z; acc[3][i].w += dx.w;
         *(float4*)(dres + row * ldr + c) = dx;
         if (dres_bf)
           *(uint2*)(dres_bf + row * ldrb + c) = make_uint2(pack_bf2(dx.x, dx.y), pack_bf2(dx.z, dx.w));
@@ -128,32 +136,31 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
     }
   }
   if (!ws) return;
-  // block reduction of the per-wave dgamma/dbeta partials, waves added in fixed order (deterministic)
+  // block reduction of the per-wave partials, waves added in fixed order (deterministic)
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        const int c = (i * 64 + lane) * 4;
-        if (c < D) {
-          float4* a = (float4*)&red[0][c];
-          float4* b = (float4*)&red[1][c];
-          if (w == 0) {
-            *a = dg[i];
-            *b = db[i];
-          } else {
-            const float4 x = *a, y = *b;
-            *a = make_float4(x.x + dg[i].x, x.y + dg[i].y, x.z + dg[i].z, x.w + dg[i].w);
-            *b = make_float4(y.x + db[i].x, y.y + db[i].y, y.z + db[i].z, y.w + db[i].w);
+      for (int k = 0; k < 4; ++k) {
+        if (k >= nsum) break;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int c = (i * 64 + lane) * 4;
+          if (c < D) {
+            float4* a = (float4*)&red[k][c];
+            if (w == 0) {
+              *a = acc[k][i];
+            } else {
+              const float4 v = *a;
+              *a = make_float4(v.x + acc[k][i].x, v.y + acc[k][i].y, v.z + acc[k][i].z, v.w + acc[k][i].w);
+            }
           }
         }
       }
     }
     __syncthreads();
   }
-  for (int c = threadIdx.x; c < D; c += 256) {
-    ws[(long)blockIdx.x * 2 * D + c] = red[0][c];
-    ws[(long)blockIdx.x * 2 * D + D + c] = red[1][c];
-  }
+  for (int k = 0; k < nsum; ++k)
+    for (int c = threadIdx.x; c < D; c += 256) ws[((long)blockIdx.x * nsum + k) * D + c] = red[k][c];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -618,35 +625,36 @@ extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, f
 
 extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const float* x, long ldx, const float* mean,
                                 const float* rstd, const float* gamma, const float* dres_in, long ldri, float* dres,
-                                long ldr, void* dres_bf16, long ldrb, float* dgamma, float* dbeta, float* ws,
-                                long ws_floats, void* stream) {
+                                long ldr, void* dres_bf16, long ldrb, float* dgamma, float* dbeta, float* sum_in,
+                                float* sum_out, float* ws, long ws_floats, void* stream) {
   if (M == 0) return VJ_OK;
   VJ_CHECK_ARG(D % 4 == 0 && D <= 64 * 4 * LN_MAXV, "vj_layernorm_bwd: bad D=%d", D);
+  VJ_CHECK_ARG(!sum_in || dres_in, "vj_layernorm_bwd: sum_in needs dres_in");
   const int nb = vj_layernorm_bwd_blocks(M);
-  const bool want_g = dgamma || dbeta;
-  if (want_g) {
-    VJ_CHECK_ARG(ws && ws_floats >= (long)nb * 2 * D, "vj_layernorm_bwd: workspace needs %ld floats", (long)nb * 2 * D);
+  const bool want_sums = sum_in || sum_out;
+  const int nsum = want_sums ? 4 : ((dgamma || dbeta) ? 2 : 0);
+  if (nsum) {
+    VJ_CHECK_ARG(ws && ws_floats >= (long)nb * nsum * D, "vj_layernorm_bwd: workspace needs %ld floats",
+                 (long)nb * nsum * D);
   }
   hipStream_t st = (hipStream_t)stream;
-  float* part = want_g ? ws : nullptr;
+  float* part = nsum ? ws : nullptr;
   const int nv = ln_nv(D);
-#define LNB(AC, NVV) hipLaunchKernelGGL((k_ln_bwd<AC, NVV>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part)
+#define LNB(AC, NVV) hipLaunchKernelGGL((k_ln_bwd<AC, NVV>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum)
 #define LNB_NV(AC) switch (nv) { case 1: LNB(AC, 1); break; case 2: LNB(AC, 2); break; case 4: LNB(AC, 4); break; case 6: LNB(AC, 6); break; default: LNB(AC, 8); }
   if (dres_in) { LNB_NV(true) }
   else { LNB_NV(false) }
 #undef LNB_NV
 #undef LNB
   VJ_LAUNCH_CHECK("vj_layernorm_bwd");
-  if (want_g) {
-    // partials laid out [nb][2][D]: dgamma column sums over rows of stride 2D
-    if (dgamma && dbeta)
-      hipLaunchKernelGGL(k_colsum2, dim3((2 * D + 31) / 32), dim3(1024), 0, st, nb, 2 * D, ws, 2L * D, dgamma, dbeta, D, 1);
-    else if (dgamma)
-      hipLaunchKernelGGL(k_colsum2, dim3((D + 31) / 32), dim3(1024), 0, st, nb, D, ws, 2L * D, dgamma, nullptr, D, 1);
-    else
-      hipLaunchKernelGGL(k_colsum2, dim3((D + 31) / 32), dim3(1024), 0, st, nb, D, ws + D, 2L * D, dbeta, nullptr, D, 1);
-    VJ_LAUNCH_CHECK("vj_layernorm_bwd(reduce)");
+  // partials laid out [nb][nsum][D]: column k sums over rows of stride nsum*D
+  float* outs[4] = {dgamma, dbeta, sum_in, sum_out};
+  for (int k = 0; k < nsum; ++k) {
+    if (!outs[k]) continue;
+    hipLaunchKernelGGL(k_colsum2, dim3((D + 31) / 32), dim3(1024), 0, st, nb, D, ws + (long)k * D, (long)nsum * D,
+                       outs[k], nullptr, D, 1);
   }
+  VJ_LAUNCH_CHECK("vj_layernorm_bwd(reduce)");
   return VJ_OK;
 }
 

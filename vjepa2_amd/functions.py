@@ -102,6 +102,10 @@ def block_forward(x, blk, lay, save):
     return x_out, saved
 
 
+def _bias_buf(lin):
+    return grad_buf(lin.bias) if lin.bias is not None and lin.bias.requires_grad else None
+
+
 def _bias_grad(lin, dy):
     if lin.bias is not None and lin.bias.requires_grad:
         ops.colsum(dy, grad_buf(lin.bias))
@@ -122,18 +126,16 @@ def block_backward(dxo, blk, lay, saved):
     dxo_b = ops.cast_bf16(dxo)
     # MLP
     dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_pre=pre)
-    ops.linear_wgrad(dxo_b, act, grad_buf(mlp.fc2.weight))
-    _bias_grad(mlp.fc2, dxo)
+    ops.linear_wgrad(dxo_b, act, grad_buf(mlp.fc2.weight))  # fc2 bias grad: fused into LN2 backward
     dln2 = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight))
     ops.linear_wgrad(dpre, ln2, grad_buf(mlp.fc1.weight))
     _bias_grad(mlp.fc1, dpre)
     gw, gb = _ln_grads(blk.norm2)
     dxm, dxm_b = ops.layernorm_bwd(dln2, x_mid, m2, r2, blk.norm2.weight, dres_in=dxo, dweight=gw, dbias=gb,
-                                   want_bf16=True)
-    # attention
+                                   want_bf16=True, sum_in=_bias_buf(mlp.fc2), sum_out=_bias_buf(attn.proj))
+    # attention (proj bias grad = column sums of dxm, produced above)
     do = ops.linear_dgrad(dxm_b, weight_bf16(attn.proj.weight))
     ops.linear_wgrad(dxm_b, o, grad_buf(attn.proj.weight))
-    _bias_grad(attn.proj, dxm)
     rope = None
     if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
         c, s = rope_tables(hd, x.device, lay.npos)

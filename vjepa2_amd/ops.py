@@ -184,24 +184,27 @@ def layernorm_fwd(x, weight, bias, eps, out_dtype=BF16, want_stats=True):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, weight, dres_in=None, dweight=None, dbias=None, want_bf16=False):
-    """Returns (dres f32 = dres_in + dLN/dx, optional bf16 copy). Accumulates dweight/dbias."""
+def layernorm_bwd(dy, x, mean, rstd, weight, dres_in=None, dweight=None, dbias=None, want_bf16=False, sum_in=None,
+                  sum_out=None):
+    """Returns (dres f32 = dres_in + dLN/dx, optional bf16 copy). Accumulates dweight/dbias and the
+    column sums of dres_in / dres into sum_in / sum_out (fused bias gradients)."""
     _dev(dy, x)
     M, D = x.shape
     assert dy.dtype == BF16 and dy.shape == (M, D)
+    assert sum_in is None or dres_in is not None
     dres = torch.empty(M, D, dtype=F32, device=x.device)
     dres_bf = torch.empty(M, D, dtype=BF16, device=x.device) if want_bf16 else None
+    nsum = 4 if (sum_in is not None or sum_out is not None) else (2 if (dweight is not None or dbias is not None) else 0)
     ws = None
     nws = 0
-    if dweight is not None or dbias is not None:
+    if nsum:
         from ._lib import load
 
-        nb = load().vj_layernorm_bwd_blocks(M)
-        nws = nb * 2 * D
+        nws = load().vj_layernorm_bwd_blocks(M) * nsum * D
         ws = torch.empty(nws, dtype=F32, device=x.device)
     _call("vj_layernorm_bwd", M, D, _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x"), _p(mean), _p(rstd),
-         _p(weight), _p(dres_in), dres_in.stride(0) if dres_in is not None else 0, _p(dres), D, _p(dres_bf), D,
-         _p(dweight), _p(dbias), _p(ws), nws, _stream())
+          _p(weight), _p(dres_in), dres_in.stride(0) if dres_in is not None else 0, _p(dres), D, _p(dres_bf), D,
+          _p(dweight), _p(dbias), _p(sum_in), _p(sum_out), _p(ws), nws, _stream())
     return dres, dres_bf
 
 

@@ -18,6 +18,8 @@
 // LDS images (one per tile, read both by rows and transposed): 16-B chunk index XOR-swizzled,
 //   HD=64 (128-B rows): sw(r) = (((r>>1)&1)<<2) | ((r>>2)&3);  HD=32 (64-B rows): sw(r) = (r>>2)&3.
 // Both keep ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads bank-conflict free.
+#include <type_traits>
+
 #include "vj_common.h"
 
 namespace {
@@ -134,7 +136,11 @@ __device__ __forceinline__ void stage_rows(__amdgpu_buffer_rsrc_t rs, long ld, i
   constexpr int CPR = HD / 8;          // 16-B chunks per row
   constexpr int RPP = 64 / CPR;        // rows per piece
   constexpr int PIECES = ROWS / RPP;
-  for (int p = wave; p < PIECES; p += nwaves) {
+  // nwaves is 4 at every call site: pieces wave, wave + 4, ... (fully unrolled, wave is uniform)
+#pragma unroll
+  for (int i = 0; i < (PIECES + 3) / 4; ++i) {
+    const int p = wave + 4 * i;
+    if (PIECES % 4 != 0 && p >= PIECES) break;
     const int r = p * RPP + lane / CPR;
     const int phys = lane % CPR;
     const int c = phys ^ swz<HD>(r);
@@ -142,6 +148,7 @@ __device__ __forceinline__ void stage_rows(__amdgpu_buffer_rsrc_t rs, long ld, i
     const uint32_t voff = ok ? (uint32_t)(((long)(row0 + r) * ld + c * 8) * 2) : VJ_OOB;
     dma16(rs, lds + p * 1024, voff);
   }
+  (void)nwaves;
 }
 
 // A-operand row fragment (rows rb + lane&31, k-step s): 8 bf16 at chunk 2s + (lane>>5).
@@ -197,7 +204,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   constexpr int TB = KT * HD * 2;  // bytes per K or V tile
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = blockIdx.y;
   int seq0, len, qt;
   locate(a.sg, blockIdx.x, 128, seq0, len, qt);
@@ -241,8 +248,10 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
   stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
   __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
+  // loop body with the LDS buffer index as a compile-time constant (unrolled by 2), so every LDS
+  // address is a per-lane base register plus an immediate offset
+  auto tile_iter = [&](const int kt, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value;
     const LDS_AS char* Ks = smem + cur * 2 * TB;
     const LDS_AS char* Vs = Ks + TB;
     if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
@@ -274,6 +283,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
       for (int d = 0; d < HD / 32; ++d) vf[ks][d] = tr_frag<HD>(Vs, ks * 16, d * 32, lane);
     const int kb = kt * KT;
     if (kb + KT > len) {  // ragged last tile only: keys beyond the sequence get -inf
+      asm volatile("");  // keeps the compiler from if-converting this into every tile
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -287,6 +297,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[1][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     if (__builtin_amdgcn_ballot_w64(mx > m_use + tau)) {
+      asm volatile("");  // a real (rare) branch, not if-converted into every tile
       const float m_new = fmaxf(m_use, mx);
       const float alpha = __builtin_amdgcn_exp2f((m_use - m_new) * c);
       m_use = m_new;
@@ -314,6 +325,10 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
       lt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf, lt, 0, 0, 0);
     }
     __syncthreads();
+  };
+  for (int kt0 = 0; kt0 < nkt; kt0 += 2) {
+    tile_iter(kt0, std::integral_constant<int, 0>{});
+    if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
   }
   const float l_tot = __shfl(lt[0], lane & 31, 64);  // row 0 of the ones tile lives in lanes 0..31
   const float inv = 1.f / l_tot;
@@ -359,7 +374,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   constexpr int STAGE = 2 * TB + 256;
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = blockIdx.y;
   int seq0, len, kt;
   locate(a.sg, blockIdx.x, 128, seq0, len, kt);
@@ -407,8 +422,10 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   __syncthreads();
   // Rows of queries past the sequence end are zero (DMA range check) with lse2 = delta = 0, so they
   // add exactly 0 to dV and dK; columns of keys past the end are never stored. No masks needed.
-  for (int qt = 0; qt < nqt; ++qt) {
-    const int cur = qt & 1;
+  // loop body with the LDS buffer index as a compile-time constant (unrolled by 2), so every LDS
+  // address is a per-lane base register plus an immediate offset
+  auto tile_iter = [&](const int qt, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value;
     if (qt + 1 < nqt) stage(qt + 1, smem + (cur ^ 1) * STAGE);
     const LDS_AS char* Qs = smem + cur * STAGE;
     const LDS_AS char* Ds = Qs + TB;
@@ -467,6 +484,10 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       }
     }
     __syncthreads();
+  };
+  for (int qt0 = 0; qt0 < nqt; qt0 += 2) {
+    tile_iter(qt0, std::integral_constant<int, 0>{});
+    if (qt0 + 1 < nqt) tile_iter(qt0 + 1, std::integral_constant<int, 1>{});
   }
   if (kok) {
     bf16_t* dk = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.k_off + h * HD;
@@ -499,7 +520,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   constexpr int TB = KT * HD * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = blockIdx.y;
   int seq0, len, qt;
   locate(a.sg, blockIdx.x, 128, seq0, len, qt);
@@ -533,8 +554,10 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
   stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
   __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
+  // loop body with the LDS buffer index as a compile-time constant (unrolled by 2), so every LDS
+  // address is a per-lane base register plus an immediate offset
+  auto tile_iter = [&](const int kt, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value;
     const LDS_AS char* Ks = smem + cur * 2 * TB;
     const LDS_AS char* Vs = Ks + TB;
     if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
@@ -573,14 +596,18 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
         st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][s], qf[s], st[kk], 0, 0, 0);
         dpt[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[kk][s], gf[s], dpt[kk], 0, 0, 0);
       }
+    if (ragged) {  // keys past the end -> -inf scores -> p = 0 (uniform branch, last tile only)
+      asm volatile("");  // keeps the compiler from if-converting this into every tile
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kt * KT + kk * 32 + acc_row(r, lane) >= len) st[kk][r] = -INFINITY;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = __builtin_amdgcn_exp2f(fmaf(st[kk][r], c, -lse2));
-        if (ragged && kt * KT + kk * 32 + acc_row(r, lane) >= len) p = 0.f;
-        dpt[kk][r] *= p;
-      }
+      for (int r = 0; r < 16; ++r) dpt[kk][r] *= __builtin_amdgcn_exp2f(fmaf(st[kk][r], c, -lse2));
       if (kk == 0) {
         lds_wait();
 #pragma unroll
@@ -597,6 +624,10 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
       }
     }
     __syncthreads();
+  };
+  for (int kt0 = 0; kt0 < nkt; kt0 += 2) {
+    tile_iter(kt0, std::integral_constant<int, 0>{});
+    if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
   }
   if (qok) {
     bf16_t* dq = a.dqkv + (long)(seq0 + qloc) * a.ldd + a.q_off + h * HD;

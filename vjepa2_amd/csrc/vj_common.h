@@ -67,8 +67,14 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // ----- buffer resource (SRD) for LDS-DMA loads with hardware range check -----
+// Buffer descriptor for a wave-uniform base/size. The values are forced into SGPRs: if the compiler
+// cannot prove uniformity it would wrap every buffer instruction in a readfirstlane waterfall loop.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  const unsigned long long a = (unsigned long long)base;
+  const unsigned long long lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a);
+  const unsigned long long hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(a >> 32));
+  const int n = __builtin_amdgcn_readfirstlane((int)bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(lo | (hi << 32)), (short)0, n, 0x00020000);
 }
 // 16 bytes per lane, global(rsrc + voffset) -> LDS(lds_wave_base + lane*16). Out-of-range -> zeros.
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, LDS_AS void* lds_wave_base, uint32_t voff) {

@@ -53,6 +53,8 @@ def rope_tables(hd, device, npos):
         omega = 1.0 / 10000**omega
         freq = torch.arange(npos, dtype=torch.float32)[:, None] * omega[None, :]
         t = (freq.cos().contiguous().to(device), freq.sin().contiguous().to(device))
+        if t[0].is_cuda:  # cached across streams (the target encoder runs on a side stream): make the
+            torch.cuda.current_stream().synchronize()  # one-time H2D copy complete before any stream uses it
         _ROPE_TABLES[key] = t
     return t
 

@@ -20,8 +20,9 @@ class KernelEvents:
 
     active = None
 
-    def __init__(self):
+    def __init__(self, only=None):
         self.rec = []
+        self.only = only  # None: every launch; else the set of labels to time (cheap enough for a timed region)
 
     def start(self):
         KernelEvents.active = self
@@ -42,7 +43,7 @@ class KernelEvents:
 
 def _call(fn, *args, label=None, flops=0):
     prof = KernelEvents.active
-    if prof is None:
+    if prof is None or (prof.only is not None and (label or fn) not in prof.only):
         return call(fn, *args)
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)

@@ -135,16 +135,38 @@ class JEPATrainer:
             self.reducer.install(mods)
 
     def forward_loss(self, clips, masks_enc, masks_pred, mask_index=0, npairs=None):
-        """Forward of one frames-per-clip group: returns (loss [1], z_pred, dz)."""
+        """Forward of one frames-per-clip group: returns (loss [1], z_pred, dz).
+
+        The target encoder's forward (train.py:414-418, no grad) depends only on the clips and the
+        EMA weights, so it runs on a second HIP stream concurrently with the context encoder and
+        predictor: its GEMM / attention tiles fill the CUs the ragged context-side launches leave
+        idle in their last wave of tiles. The loss waits for both."""
         B = clips.shape[0]
-        with torch.no_grad():
-            h = self.tgt.forward_features(clips)
+        side = self._side_stream()
+        if side is not None:
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)  # clips + this step's EMA'd target weights are ready
+            with torch.cuda.stream(side), torch.no_grad():
+                h = self.tgt.forward_features(clips)
+        else:
+            with torch.no_grad():
+                h = self.tgt.forward_features(clips)
         z, _ = self.enc.forward_ragged(clips, masks_enc, out_dtype=torch.bfloat16)
         zp, pl = self.pred.forward_ragged(z, masks_enc, masks_pred, mask_index=mask_index, out_dtype=torch.bfloat16)
+        if side is not None:
+            main.wait_stream(side)
+            h.record_stream(main)
         loss, dz, _ = ops.jepa_loss(zp, h, pl.loss_rows, self.tgt.norm.weight, self.tgt.norm.bias,
                                     [B * int(m.shape[1]) for m in masks_pred], eps1=self.tgt.norm.eps, eps2=1e-5,
                                     loss_exp=self.loss_exp, npairs=npairs)
         return loss, zp, dz
+
+    def _side_stream(self):
+        if os.environ.get("VJ_TGT_STREAM", "1") == "0" or not torch.cuda.is_available():
+            return None
+        if getattr(self, "_tgt_stream", None) is None:
+            self._tgt_stream = torch.cuda.Stream()
+        return self._tgt_stream
 
     def train_step(self, clips, masks_enc, masks_pred, momentum):
         """clips / masks_* are per frames-per-clip group lists (train.py:393-400 layout). LR / WD

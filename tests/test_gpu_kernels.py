@@ -132,6 +132,24 @@ def test_gemm_epilogues(M, N):
     _close(dw, exp, 2e-4 * math.sqrt(M), 1e-5, "wgrad accumulate")
 
 
+@pytest.mark.parametrize("knobs", [dict(VJ_GEMM_PXCD="1"), dict(VJ_GEMM_PXCD="3", VJ_GEMM_GROUP="3")])
+def test_gemm_persistent_walk(knobs, monkeypatch):
+    """The 256-row kernel is persistent: with few blocks per XCD every block walks many tiles, which
+    exercises the next-tile DMA hand-off (slot parity for odd K-tile counts, K <= 64 single-tile,
+    ragged tails) for every layout and epilogue, plus the grouped tile order."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    for shape in [(2100, 768, 320), (1500, 384, 64), (1030, 1160, 128), (2048, 1024, 200)]:
+        for ak in (True, False):
+            for bk in (True, False):
+                test_gemm_layouts(ak, bk, shape)
+    for M, N in [(1333, 256), (1333, 384), (1333, 200)]:
+        test_gemm_epilogues(M, N)
+    test_gemm_splitk(2, (520, 392, 3000))
+    test_gemm_splitk(0, (512, 256, 4100))
+    test_fused_rope_paths(1500, 64, 2)
+
+
 # ------------------------------------------------------------------------------------------------
 def _attn_ref(q, k, v, groups, scale):
     """q,k,v f32 [T, H, hd] (concatenated sequences) -> O [T,H,hd], lse [H,T]"""

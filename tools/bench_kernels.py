@@ -1,9 +1,12 @@
 """A/B timing of GEMM / attention kernel builds in ONE process (interleaved rounds, median).
 
-usage: python tools/bench_kernels.py [lib.so ...]   (default: vjepa2_amd/libvjepa_hip.so)
-Builds come from `python -m vjepa2_amd.build --variant NAME -DMACRO=...`. Random operands
-(uniform [-1, 1) scaled), shapes of the ViT-L/16 B=24 train step.
+usage: python tools/bench_kernels.py [COL ...]   COL = lib.so | lib.so@ENV=V[,ENV2=V2] | @ENV=V
+(default: vjepa2_amd/libvjepa_hip.so). Builds come from `python -m vjepa2_amd.build --variant NAME
+-DMACRO=...`; an @ENV column times a build under host-side knobs (VJ_GEMM_GROUP, VJ_GEMM_PXCD), set
+only while that column runs. Random operands (uniform [-1, 1) scaled), shapes of the ViT-L/16 B=24
+train step.
 """
+import contextlib
 import ctypes
 import os
 import statistics
@@ -47,6 +50,13 @@ GEMMS = [
     ("pred fc1", 71232, 1536, 384, 1, 1, 3, 1),
     ("pred fc2", 71232, 384, 1536, 1, 1, 2, 1),
 ]
+
+
+ATTN = [("attn fwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], False),
+        ("attn fwd hd64 tgt", 64, 16, [(24, 2048)], False),
+        ("attn bwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], True),
+        ("attn fwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], False),
+        ("attn bwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], True)]
 
 
 def gemm_case(lib, case, dev, stream):
@@ -110,8 +120,29 @@ def time_fn(fn, iters=10):
     return s.elapsed_time(e) / iters
 
 
+def parse_col(arg):
+    path, _, env = arg.partition("@")
+    envs = dict(kv.split("=", 1) for kv in env.split(",") if kv)
+    return (path or os.path.join(HERE, "vjepa2_amd", "libvjepa_hip.so")), envs
+
+
+@contextlib.contextmanager
+def env_set(envs):
+    old = {k: os.environ.get(k) for k in envs}
+    os.environ.update(envs)
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def main():
-    paths = [a for a in sys.argv[1:] if a.endswith(".so")] or [os.path.join(HERE, "vjepa2_amd", "libvjepa_hip.so")]
+    cols = [parse_col(a) for a in sys.argv[1:]] or [parse_col("")]
+    paths = [p for p, _ in cols]
     rounds = int(os.environ.get("VJ_BENCH_ROUNDS", "7"))
     dev = torch.device("cuda")
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -122,26 +153,23 @@ def main():
         if only and only not in c[0]:
             continue
         cases.append((c[0], [gemm_case(lib, c, dev, stream) for lib in libs]))
-    attn = [("attn fwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], False),
-            ("attn fwd hd64 tgt", 64, 16, [(24, 2048)], False),
-            ("attn bwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], True),
-            ("attn fwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], False),
-            ("attn bwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], True)]
-    for name, hd, H, groups, bwd in attn:
+    for name, hd, H, groups, bwd in ATTN:
         if only and only not in name:
             continue
         cases.append((name, [attn_case(lib, hd, H, groups, dev, stream, bwd) for lib in libs]))
-    print(f"{'case':22s} " + " ".join(f"{os.path.basename(pth)[:24]:>26s}" for pth in paths), flush=True)
+    names = [os.path.basename(p).replace("libvjepa_hip", "lib")[:14] + ("@" + ",".join(f"{k[7:] if k.startswith('VJ_GEMM_') else k}={v}" for k, v in e.items()) if e else "") for p, e in cols]
+    print(f"{'case':22s} " + " ".join(f"{n[:26]:>26s}" for n in names), flush=True)
     for name, runs in cases:
         res = [[] for _ in libs]
         for _ in range(rounds):
             for i, (fn, fl) in enumerate(runs):
-                res[i].append(time_fn(fn))
-        cols = []
+                with env_set(cols[i][1]):
+                    res[i].append(time_fn(fn))
+        out = []
         for i, (fn, fl) in enumerate(runs):
             ms = statistics.median(res[i])
-            cols.append(f"{ms * 1e3:9.1f}us {fl / ms / 1e9:7.1f}TF")
-        print(f"{name:22s} " + " ".join(f"{c:>26s}" for c in cols), flush=True)
+            out.append(f"{ms * 1e3:9.1f}us {fl / ms / 1e9:7.1f}TF")
+        print(f"{name:22s} " + " ".join(f"{c:>26s}" for c in out), flush=True)
 
 
 if __name__ == "__main__":

@@ -10,7 +10,8 @@ import os
 
 import torch  # noqa: F401  (loads the HIP runtime our library links against)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvjepa_hip.so")
+# VJ_LIB: an alternative build of the same library (A/B timing of kernel variants, tools/)
+LIB_PATH = os.environ.get("VJ_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libvjepa_hip.so")
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

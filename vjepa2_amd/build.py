@@ -21,6 +21,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # epilogue VALU reads them in place instead of through v_accvgpr_read/write copies.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-mcode-object-version=5",
           "-mllvm", "-amdgpu-mfma-vgpr-form=1", "-Wno-unused-command-line-argument"]
+# Per-source extra flags. Attention: no SLP packing of the softmax f32 math (v_pk_mul_f32 beside
+# MFMAs costs issue slots and forces v_mov / v_alignbit shuffles before the bf16 packs).
+SRC_FLAGS = {"vj_attn.hip": ["-fno-slp-vectorize"]}
 
 
 def _torch_libdir():
@@ -69,7 +72,7 @@ def build(verbose=True, force=False, variant=None, defines=()):
         src = os.path.join(csrc, s)
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
         if force or variant or _needs_build(obj, src, gen):
-            jobs.append([HIPCC, *flags, "-c", src, "-o", obj])
+            jobs.append([HIPCC, *flags, *SRC_FLAGS.get(s, []), "-c", src, "-o", obj])
 
     def run(cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)

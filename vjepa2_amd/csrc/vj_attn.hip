@@ -22,6 +22,20 @@
 
 #include "vj_common.h"
 
+// 32-row key (dK/dV sweep) and query (dQ sweep) tiles per wave, per head dim
+#ifndef VJ_ATTN_KW32
+#define VJ_ATTN_KW32 2
+#endif
+#ifndef VJ_ATTN_QW32
+#define VJ_ATTN_QW32 2
+#endif
+#ifndef VJ_ATTN_KW64
+#define VJ_ATTN_KW64 1
+#endif
+#ifndef VJ_ATTN_QW64
+#define VJ_ATTN_QW64 1
+#endif
+
 namespace {
 
 constexpr int MAXG = 4;
@@ -41,7 +55,7 @@ struct AttnArgs {
   long ldo;
   const bf16_t* dout;  // backward: dO
   long lddo;
-  float* stats;  // [2][H][T]: lse2 = log2(sum_k 2^(scale*log2e*s_k)), delta = rowsum(dO*O)
+  float* stats;  // [2][H][T]: lse2 = log2(sum_k 2^(scale*log2e*s_k)), -delta = -rowsum(dO*O)
   bf16_t* dqkv;  // backward output, same layout as qkv
   long ldd;
   int H, T;
@@ -346,7 +360,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// delta[h][t] = sum_d dO[t][h*hd+d] * O[t][h*hd+d]   (one thread per (token, head))
+// -delta[h][t] = -sum_d dO[t][h*hd+d] * O[t][h*hd+d]   (one thread per (token, head))
 template <int HD>
 __global__ void k_attn_delta(AttnArgs a) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -361,12 +375,14 @@ __global__ void k_attn_delta(AttnArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += (float)x[j] * (float)y[j];
   }
-  a.stats[(long)a.H * a.T + (long)h * a.T + t] = s;
+  a.stats[(long)a.H * a.T + (long)h * a.T + t] = -s;  // stored negated: the backward's initial dP accumulator
 }
 
 // ------------------------------------------------------------------------------------------------
-// dK/dV: block = 4 waves x 32 keys; sweep query tiles of 32 (Q, dO, lse, delta staged in LDS).
-template <int HD>
+// dK/dV: block = 4 waves x (32 KW) keys; sweep query tiles of 32 (Q, dO, lse, delta staged in LDS).
+// Each wave owns KW 32-key tiles (key tile kw of wave w: keys kw*128 + w*32 + 0..31 of the block),
+// so every staged Q / dO fragment feeds KW independent MFMA chains per barrier.
+template <int HD, int KW>
 __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   constexpr int QT = 32;
   constexpr int TB = QT * HD * 2;
@@ -377,19 +393,27 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = blockIdx.y;
   int seq0, len, kt;
-  locate(a.sg, blockIdx.x, 128, seq0, len, kt);
-  const int kloc = kt * 128 + wave * 32 + (lane & 31);
-  const bool kok = kloc < len;
+  locate(a.sg, blockIdx.x, 128 * KW, seq0, len, kt);
+  int kloc[KW];
+  bool kok[KW];
+#pragma unroll
+  for (int kw = 0; kw < KW; ++kw) {
+    kloc[kw] = kt * 128 * KW + kw * 128 + wave * 32 + (lane & 31);
+    kok[kw] = kloc[kw] < len;
+  }
   const int hl = lane >> 5;
 
   // K^T and V^T fragments (B operands): lane holds K[key][16s + 8h + j].
-  bf16x8 kf[HD / 16], vf[HD / 16];
-  const bf16_t* krow = a.qkv + (long)(seq0 + kloc) * a.ld + a.k_off + h * HD;
-  const bf16_t* vrow = a.qkv + (long)(seq0 + kloc) * a.ld + a.v_off + h * HD;
+  bf16x8 kf[KW][HD / 16], vf[KW][HD / 16];
 #pragma unroll
-  for (int s = 0; s < HD / 16; ++s) {
-    kf[s] = gload8(krow + 16 * s + 8 * hl, kok);
-    vf[s] = gload8(vrow + 16 * s + 8 * hl, kok);
+  for (int kw = 0; kw < KW; ++kw) {
+    const bf16_t* krow = a.qkv + (long)(seq0 + kloc[kw]) * a.ld + a.k_off + h * HD;
+    const bf16_t* vrow = a.qkv + (long)(seq0 + kloc[kw]) * a.ld + a.v_off + h * HD;
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) {
+      kf[kw][s] = gload8(krow + 16 * s + 8 * hl, kok[kw]);
+      vf[kw][s] = gload8(vrow + 16 * s + 8 * hl, kok[kw]);
+    }
   }
   const uint32_t qbytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
   const uint32_t dbytes = (uint32_t)min((long)len * a.lddo * 2, 0x7fffffffL);
@@ -400,12 +424,15 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       make_rsrc(a.stats + (long)h * a.T + seq0, (uint32_t)min(((long)a.H * a.T + len) * 4, 0x7fffffffL));
   const long dstat = (long)a.H * a.T;  // element distance lse -> delta
 
-  f32x16 dvt[HD / 32], dkt[HD / 32];
+  f32x16 dvt[KW][HD / 32], dkt[KW][HD / 32];
 #pragma unroll
-  for (int d = 0; d < HD / 32; ++d)
+  for (int kw = 0; kw < KW; ++kw)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dvt[d][r] = dkt[d][r] = 0.f;
+    for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dvt[kw][d][r] = dkt[kw][d][r] = 0.f;
   const float c = a.scale * LOG2E;
+  const float rc = -1.f / c;
 
   auto stage = [&](int qt, LDS_AS char* st) {
     stage_rows<HD, QT>(rq, a.ld, qt * QT, len, st, wave, lane, 4);
@@ -436,21 +463,26 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       qa[s] = row_frag<HD>(Qs, 0, s, lane);
       da[s] = row_frag<HD>(Ds, 0, s, lane);
     }
-    // S = Q K^T (rows: queries, col: key); dP - delta = dO V^T - delta (delta as the initial acc)
-    f32x16 sacc, dp;
-    float l2[16];
+    // S - lse2/c = Q K^T - lse2/c (rows: queries, col: key); dP - delta = dO V^T - delta: the
+    // per-query terms are the accumulators' initial values, so no per-row registers stay live
+    f32x16 sacc[KW], dp[KW];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = acc_row(r, lane);
-      l2[r] = Ls[qi];
-      dp[r] = -Ls[32 + qi];
-      sacc[r] = 0.f;
+      const float l2 = Ls[qi] * rc, dl = Ls[32 + qi];
+#pragma unroll
+      for (int kw = 0; kw < KW; ++kw) {
+        sacc[kw][r] = l2;
+        dp[kw][r] = dl;
+      }
     }
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s) {
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[s], sacc, 0, 0, 0);
-      dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[s], dp, 0, 0, 0);
-    }
+    for (int s = 0; s < HD / 16; ++s)
+#pragma unroll
+      for (int kw = 0; kw < KW; ++kw) {
+        sacc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[kw][s], sacc[kw], 0, 0, 0);
+        dp[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[kw][s], dp[kw], 0, 0, 0);
+      }
     bf16x8 dtf[2][HD / 32], qtf[2][HD / 32];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -461,11 +493,13 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       }
     // P = 2^(c*S - lse2); dS = P * (dP - delta)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = __builtin_amdgcn_exp2f(fmaf(sacc[r], c, -l2[r]));
-      sacc[r] = p;
-      dp[r] *= p;
-    }
+    for (int kw = 0; kw < KW; ++kw)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(sacc[kw][r] * c);
+        sacc[kw][r] = p;
+        dp[kw][r] *= p;
+      }
     // dV^T += dO^T P ; dK^T += Q^T dS   (k-permuted accumulators as B operands)
     lds_wait();
 #pragma unroll
@@ -474,47 +508,53 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       tie(qtf[s2]);
     }
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bf16x8 pf = acc_frag(sacc, s2);
-      const bf16x8 sf = acc_frag(dp, s2);
+    for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int d = 0; d < HD / 32; ++d) {
-        dvt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dtf[s2][d], pf, dvt[d], 0, 0, 0);
-        dkt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtf[s2][d], sf, dkt[d], 0, 0, 0);
+      for (int kw = 0; kw < KW; ++kw) {
+        const bf16x8 pf = acc_frag(sacc[kw], s2);
+        const bf16x8 sf = acc_frag(dp[kw], s2);
+#pragma unroll
+        for (int d = 0; d < HD / 32; ++d) {
+          dvt[kw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dtf[s2][d], pf, dvt[kw][d], 0, 0, 0);
+          dkt[kw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtf[s2][d], sf, dkt[kw][d], 0, 0, 0);
+        }
       }
-    }
     __syncthreads();
   };
   for (int qt0 = 0; qt0 < nqt; qt0 += 2) {
     tile_iter(qt0, std::integral_constant<int, 0>{});
     if (qt0 + 1 < nqt) tile_iter(qt0 + 1, std::integral_constant<int, 1>{});
   }
-  if (kok) {
-    bf16_t* dk = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.k_off + h * HD;
-    bf16_t* dv = a.dqkv + (long)(seq0 + kloc) * a.ldd + a.v_off + h * HD;
+#pragma unroll
+  for (int kw = 0; kw < KW; ++kw) {
+    if (!kok[kw]) continue;
+    bf16_t* dk = a.dqkv + (long)(seq0 + kloc[kw]) * a.ldd + a.k_off + h * HD;
+    bf16_t* dv = a.dqkv + (long)(seq0 + kloc[kw]) * a.ldd + a.v_off + h * HD;
     const bool rope = a.cos_t != nullptr;
-    const TokPos tp = rope ? tok_pos(a, seq0 + kloc) : TokPos{0, 0, 0};
+    const TokPos tp = rope ? tok_pos(a, seq0 + kloc[kw]) : TokPos{0, 0, 0};
     // rotate everything before the first store (the stores could alias the tables, so the
     // table loads would otherwise be serialised behind them)
 #pragma unroll
     for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dkt[d][r] *= a.scale;
-    if (rope) rope_inv_rows<HD>(a, tp, lane, dkt);
+      for (int r = 0; r < 16; ++r) dkt[kw][d][r] *= a.scale;
+    if (rope) rope_inv_rows<HD>(a, tp, lane, dkt[kw]);
 #pragma unroll
     for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int col = d * 32 + acc_row(r, lane);
-        *(uint32_t*)(dk + col) = pack_bf2(dkt[d][r], dkt[d][r + 1]);
-        *(uint32_t*)(dv + col) = pack_bf2(dvt[d][r], dvt[d][r + 1]);
+        *(uint32_t*)(dk + col) = pack_bf2(dkt[kw][d][r], dkt[kw][d][r + 1]);
+        *(uint32_t*)(dv + col) = pack_bf2(dvt[kw][d][r], dvt[kw][d][r + 1]);
       }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// dQ: block = 4 waves x 32 queries; sweep key tiles of 64 (K, V staged in LDS).
-template <int HD>
+// dQ: block = 4 waves x (32 QW) queries; sweep key tiles of 64 (K, V staged in LDS). Each wave owns
+// QW 32-query tiles (tile qw of wave w: queries qw*128 + w*32 + 0..31 of the block), so every K / V
+// fragment read from LDS feeds QW independent MFMA chains.
+template <int HD, int QW>
 __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   constexpr int KT = 64;
   constexpr int TB = KT * HD * 2;
@@ -523,32 +563,42 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int h = blockIdx.y;
   int seq0, len, qt;
-  locate(a.sg, blockIdx.x, 128, seq0, len, qt);
-  const int qloc = qt * 128 + wave * 32 + (lane & 31);
-  const bool qok = qloc < len;
+  locate(a.sg, blockIdx.x, 128 * QW, seq0, len, qt);
   const int hl = lane >> 5;
-
-  bf16x8 qf[HD / 16], gf[HD / 16];
-  const bf16_t* qrow = a.qkv + (long)(seq0 + qloc) * a.ld + a.q_off + h * HD;
-  const bf16_t* grow = a.dout + (long)(seq0 + qloc) * a.lddo + h * HD;
+  int qloc[QW];
+  bool qok[QW];
+  bf16x8 qf[QW][HD / 16], gf[QW][HD / 16];
+  float lse2[QW], dl[QW];
 #pragma unroll
-  for (int s = 0; s < HD / 16; ++s) {
-    qf[s] = gload8(qrow + 16 * s + 8 * hl, qok);
-    gf[s] = gload8(grow + 16 * s + 8 * hl, qok);
+  for (int qw = 0; qw < QW; ++qw) {
+    qloc[qw] = qt * 128 * QW + qw * 128 + wave * 32 + (lane & 31);
+    qok[qw] = qloc[qw] < len;
+    const bf16_t* qrow = a.qkv + (long)(seq0 + qloc[qw]) * a.ld + a.q_off + h * HD;
+    const bf16_t* grow = a.dout + (long)(seq0 + qloc[qw]) * a.lddo + h * HD;
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s) {
+      qf[qw][s] = gload8(qrow + 16 * s + 8 * hl, qok[qw]);
+      gf[qw][s] = gload8(grow + 16 * s + 8 * hl, qok[qw]);
+    }
+    lse2[qw] = qok[qw] ? a.stats[(long)h * a.T + seq0 + qloc[qw]] : 0.f;
+    dl[qw] = qok[qw] ? a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc[qw]] : 0.f;
   }
-  const float lse2 = qok ? a.stats[(long)h * a.T + seq0 + qloc] : 0.f;
-  const float dl = qok ? a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc] : 0.f;
 
   const uint32_t bytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
   const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.qkv + (long)seq0 * a.ld + a.k_off + h * HD, bytes);
   const __amdgpu_buffer_rsrc_t rv = make_rsrc(a.qkv + (long)seq0 * a.ld + a.v_off + h * HD, bytes);
 
-  f32x16 dqt[HD / 32];
+  f32x16 dqt[QW][HD / 32];
 #pragma unroll
-  for (int d = 0; d < HD / 32; ++d)
+  for (int qw = 0; qw < QW; ++qw)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) dqt[d][r] = 0.f;
+    for (int d = 0; d < HD / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dqt[qw][d][r] = 0.f;
   const float c = a.scale * LOG2E;
+  float nl2[QW];  // -lse2 / c: initial value of the S^T accumulators, so p = 2^(c * acc)
+#pragma unroll
+  for (int qw = 0; qw < QW; ++qw) nl2[qw] = -lse2[qw] / c;
 
   const int nkt = (len + KT - 1) / KT;
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
@@ -565,63 +615,62 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
       stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
       stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
     }
-    bf16x8 ka[2][HD / 16], va[2][HD / 16], ktf[2][2][HD / 32];
+    const bool ragged = (kt + 1) * KT > len;
+    // Per 32-key half kk: S^T = K Q^T and dP^T - delta = V dO^T - delta for the QW query tiles, then
+    // dQ^T += K^T dS^T. Halves run one after the other so only one half's fragments are live.
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 ka[HD / 16], va[HD / 16], ktf[2][HD / 32];
 #pragma unroll
       for (int s = 0; s < HD / 16; ++s) {
-        ka[kk][s] = row_frag<HD>(Ks, kk * 32, s, lane);
-        va[kk][s] = row_frag<HD>(Vs, kk * 32, s, lane);
+        ka[s] = row_frag<HD>(Ks, kk * 32, s, lane);
+        va[s] = row_frag<HD>(Vs, kk * 32, s, lane);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int d = 0; d < HD / 32; ++d) ktf[kk][s2][d] = tr_frag<HD>(Ks, kk * 32 + s2 * 16, d * 32, lane);
-    }
-    // keys past the end are zero rows of K and V; masked on the ragged last tile only so an extreme
-    // lse cannot turn 2^(-lse2) * 0 into inf * 0
-    const bool ragged = (kt + 1) * KT > len;
-    f32x16 st[2], dpt[2];
+        for (int d = 0; d < HD / 32; ++d) ktf[s2][d] = tr_frag<HD>(Ks, kk * 32 + s2 * 16, d * 32, lane);
+      f32x16 st[QW], dpt[QW];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+      for (int qw = 0; qw < QW; ++qw)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        st[kk][r] = 0.f;
-        dpt[kk][r] = -dl;
+        for (int r = 0; r < 16; ++r) {
+          st[qw][r] = nl2[qw];
+          dpt[qw][r] = dl[qw];
+        }
+#pragma unroll
+      for (int s = 0; s < HD / 16; ++s)
+#pragma unroll
+        for (int qw = 0; qw < QW; ++qw) {
+          st[qw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s], qf[qw][s], st[qw], 0, 0, 0);
+          dpt[qw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s], gf[qw][s], dpt[qw], 0, 0, 0);
+        }
+      // keys past the end are zero rows of K and V; masked on the ragged last tile only so an
+      // extreme lse cannot turn 2^(-lse2) * 0 into inf * 0
+      if (ragged) {  // uniform branch, last tile only
+        asm volatile("");  // keeps the compiler from if-converting this into every tile
+#pragma unroll
+        for (int qw = 0; qw < QW; ++qw)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kt * KT + kk * 32 + acc_row(r, lane) >= len) st[qw][r] = -INFINITY;
       }
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s)
+      for (int qw = 0; qw < QW; ++qw)
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[kk][s], qf[s], st[kk], 0, 0, 0);
-        dpt[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[kk][s], gf[s], dpt[kk], 0, 0, 0);
-      }
-    if (ragged) {  // keys past the end -> -inf scores -> p = 0 (uniform branch, last tile only)
-      asm volatile("");  // keeps the compiler from if-converting this into every tile
+        for (int r = 0; r < 16; ++r) dpt[qw][r] *= __builtin_amdgcn_exp2f(st[qw][r] * c);
+      lds_wait();
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int s2 = 0; s2 < 2; ++s2) tie(ktf[s2]);
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kt * KT + kk * 32 + acc_row(r, lane) >= len) st[kk][r] = -INFINITY;
-    }
+      for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+        for (int qw = 0; qw < QW; ++qw) {
+          const bf16x8 sf = acc_frag(dpt[qw], s2);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dpt[kk][r] *= __builtin_amdgcn_exp2f(fmaf(st[kk][r], c, -lse2));
-      if (kk == 0) {
-        lds_wait();
-#pragma unroll
-        for (int k2 = 0; k2 < 2; ++k2)
-#pragma unroll
-          for (int s2 = 0; s2 < 2; ++s2) tie(ktf[k2][s2]);
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {
-        const bf16x8 sf = acc_frag(dpt[kk], s2);
-#pragma unroll
-        for (int d = 0; d < HD / 32; ++d)
-          dqt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktf[kk][s2][d], sf, dqt[d], 0, 0, 0);
-      }
+          for (int d = 0; d < HD / 32; ++d)
+            dqt[qw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktf[s2][d], sf, dqt[qw][d], 0, 0, 0);
+        }
     }
     __syncthreads();
   };
@@ -629,20 +678,22 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
     tile_iter(kt0, std::integral_constant<int, 0>{});
     if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
   }
-  if (qok) {
-    bf16_t* dq = a.dqkv + (long)(seq0 + qloc) * a.ldd + a.q_off + h * HD;
+#pragma unroll
+  for (int qw = 0; qw < QW; ++qw) {
+    if (!qok[qw]) continue;
+    bf16_t* dq = a.dqkv + (long)(seq0 + qloc[qw]) * a.ldd + a.q_off + h * HD;
     const bool rope = a.cos_t != nullptr;
-    const TokPos tp = rope ? tok_pos(a, seq0 + qloc) : TokPos{0, 0, 0};
+    const TokPos tp = rope ? tok_pos(a, seq0 + qloc[qw]) : TokPos{0, 0, 0};
 #pragma unroll
     for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dqt[d][r] *= a.scale;
-    if (rope) rope_inv_rows<HD>(a, tp, lane, dqt);  // rotate first, then store (see k_attn_bwd_dkdv)
+      for (int r = 0; r < 16; ++r) dqt[qw][d][r] *= a.scale;
+    if (rope) rope_inv_rows<HD>(a, tp, lane, dqt[qw]);  // rotate first, then store (see k_attn_bwd_dkdv)
 #pragma unroll
     for (int d = 0; d < HD / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; r += 2)
-        *(uint32_t*)(dq + d * 32 + acc_row(r, lane)) = pack_bf2(dqt[d][r], dqt[d][r + 1]);
+        *(uint32_t*)(dq + d * 32 + acc_row(r, lane)) = pack_bf2(dqt[qw][d][r], dqt[qw][d][r + 1]);
   }
 }
 
@@ -721,20 +772,26 @@ extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q
   a.qkv = (const bf16_t*)qkv; a.ld = ld; a.q_off = q_off; a.k_off = k_off; a.v_off = v_off;
   a.o = (bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.stats = stats;
   a.dqkv = (bf16_t*)dqkv; a.ldd = ldd; a.H = H; a.T = T; a.scale = scale;
-  rc = fill_groups(a.sg, ngroups, nseq, len, 128, T);
+  // key / query 32-row tiles per wave of the two sweeps (block tile = 128 x that)
+  const int kw = hd == 64 ? VJ_ATTN_KW64 : VJ_ATTN_KW32;
+  const int qw = hd == 64 ? VJ_ATTN_QW64 : VJ_ATTN_QW32;
+  AttnArgs ak = a, aq = a;
+  rc = fill_groups(ak.sg, ngroups, nseq, len, 128 * kw, T);
+  if (rc) return rc;
+  rc = fill_groups(aq.sg, ngroups, nseq, len, 128 * qw, T);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
   const long nth = (long)T * H;
   const int dblocks = (int)((nth + 255) / 256);
-  dim3 grid(a.sg.tiles_prefix[MAXG], H);
+  const dim3 gk(ak.sg.tiles_prefix[MAXG], H), gq(aq.sg.tiles_prefix[MAXG], H);
   if (hd == 64) {
     hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_attn_bwd_dkdv<64>, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_attn_bwd_dq<64>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64>), gk, dim3(256), 0, st, ak);
+    hipLaunchKernelGGL((k_attn_bwd_dq<64, VJ_ATTN_QW64>), gq, dim3(256), 0, st, aq);
   } else {
     hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_attn_bwd_dkdv<32>, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_attn_bwd_dq<32>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32>), gk, dim3(256), 0, st, ak);
+    hipLaunchKernelGGL((k_attn_bwd_dq<32, VJ_ATTN_QW32>), gq, dim3(256), 0, st, aq);
   }
   VJ_LAUNCH_CHECK("vj_attn_bwd");
   return VJ_OK;

@@ -166,6 +166,30 @@ def main():
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
                 "launches_per_step": st["count"] / args.steps, "avg_launch_us": round(st["total_ms"] * 1e3 / st["count"], 2),
                 "flops_per_launch": st["flops"] / st["count"]}
+        tr = _pmc_traffic(dom)
+        if tr:
+            roof["traffic"] = tr["hbm_bytes_per_launch"]
+            roof["traffic_unit"] = "B/launch"
+            roof["traffic_source"] = tr["source"]
+
+    # The target encoder's forward runs on a side stream (train.py), so inside the timed region the
+    # dominant kernel shares the CUs with it and its launch durations include that sharing. One more
+    # UNTIMED step with the side stream off gives the same kernel's unshared launch duration.
+    if roof and os.environ.get("VJ_TGT_STREAM", "1") != "0":
+        solo = ops.KernelEvents(only={dom})
+        os.environ["VJ_TGT_STREAM"] = "0"
+        torch.cuda.synchronize()
+        solo.start()
+        run(nsteps - 1)
+        solo.stop()
+        torch.cuda.synchronize()
+        del os.environ["VJ_TGT_STREAM"]
+        st1 = solo.summary()[dom]
+        a1 = st1["flops"] / (st1["total_ms"] * 1e-3) / 1e12
+        roof["timed_region_shares_cus_with"] = "target-encoder side stream"
+        roof["unshared"] = {"achieved": round(a1, 1), "frac": round(a1 / PEAK_BF16_TFLOPS, 4),
+                            "avg_launch_us": round(st1["total_ms"] * 1e3 / st1["count"], 2),
+                            "measured": "one extra untimed step, target encoder on the main stream"}
 
     cpu = None
     if rank == 0 and args.cpu_baseline:
@@ -190,6 +214,21 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _pmc_traffic(label):
+    """HBM bytes per launch of `label` measured by rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) over
+    this same bench, reduced by tools/traffic.py into profiles/traffic.json; None if the committed
+    measurement is for another kernel."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
+    try:
+        tr = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if tr.get("kernel") != label:
+        return None
+    tr["source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py)"
+    return tr
 
 
 def cpu_baseline(args, sample):

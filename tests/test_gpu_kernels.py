@@ -192,6 +192,34 @@ def test_attention_fwd_bwd(hd, H, groups):
     assert torch.equal(dqkv, dqkv2)
 
 
+@pytest.mark.parametrize("hd", [64, 32])
+def test_attention_rescale_spikes(hd):
+    """Score maxima that grow tile after tile (every step takes the lazy-rescale branch) and one
+    isolated spike key per sequence: exercises the O/l rescale of the pipelined forward."""
+    from vjepa2_amd import ops
+
+    H, groups = 2, [(2, 300), (1, 77)]
+    T = sum(n * l for n, l in groups)
+    D = H * hd
+    g = torch.Generator(device="cpu").manual_seed(7 * hd)
+    qkv = torch.randn(T, 3 * D, generator=g)
+    t0 = 0
+    for ns, ln in groups:
+        for _ in range(ns):
+            ramp = torch.linspace(0.5, 6.0, ln).unsqueeze(1)
+            qkv[t0:t0 + ln, D:2 * D] *= ramp  # keys grow with position -> max rises every tile
+            qkv[t0 + ln // 2, D:2 * D] = qkv[t0, :D] * 8.0  # spike aligned with the first query
+            t0 += ln
+    qkv = qkv.to(DEV).bfloat16()
+    scale = hd ** -0.5
+    o, stats = ops.attn_fwd(qkv, H, hd, groups, scale)
+    q, k, v = (qkv[:, i * D:(i + 1) * D].float().reshape(T, H, hd) for i in range(3))
+    o_ref, lse_ref = _attn_ref(q, k, v, groups, scale)
+    torch.cuda.synchronize()
+    _close(o.reshape(T, H, hd), o_ref, 1e-2, 2e-2, f"attn spikes fwd hd={hd}")
+    _close(stats[0] * math.log(2.0), lse_ref, 2e-3, 1e-4, f"attn spikes lse hd={hd}")
+
+
 # ------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("D", [64, 384, 1024, 1408])
 def test_layernorm(D):

@@ -125,7 +125,8 @@ def block_backward(dxo, blk, lay, saved):
     T, D = x.shape
     H = attn.num_heads
     hd = D // H
-    dxo_b = ops.cast_bf16(dxo)
+    twin = getattr(dxo, "_vj_grad_bf16", None)  # bf16 twin written by the next block's LN1 backward,
+    dxo_b = twin[0] if twin is not None and twin[1] == dxo._version else ops.cast_bf16(dxo)  # unless changed since
     # MLP
     dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_pre=pre)
     ops.linear_wgrad(dxo_b, act, grad_buf(mlp.fc2.weight))  # fc2 bias grad: fused into LN2 backward
@@ -147,7 +148,9 @@ def block_backward(dxo, blk, lay, saved):
     ops.linear_wgrad(dqkv, ln1, grad_buf(attn.qkv.weight))
     _bias_grad(attn.qkv, dqkv)
     gw, gb = _ln_grads(blk.norm1)
-    dxi, _ = ops.layernorm_bwd(dln1, x, m1, r1, blk.norm1.weight, dres_in=dxm, dweight=gw, dbias=gb)
+    dxi, dxi_b = ops.layernorm_bwd(dln1, x, m1, r1, blk.norm1.weight, dres_in=dxm, dweight=gw, dbias=gb,
+                                   want_bf16=True)
+    dxi._vj_grad_bf16 = (dxi_b, dxi._version)  # the previous block's fc2 dgrad / wgrad operand (saves a cast)
     return dxi
 
 

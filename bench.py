@@ -166,7 +166,7 @@ def main():
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
                 "launches_per_step": st["count"] / args.steps, "avg_launch_us": round(st["total_ms"] * 1e3 / st["count"], 2),
                 "flops_per_launch": st["flops"] / st["count"]}
-        tr = _pmc_traffic(dom)
+        tr = _pmc_traffic(dom, f"{args.model} {T}x{S}^2 B={B}")
         if tr:
             roof["traffic"] = tr["hbm_bytes_per_launch"]
             roof["traffic_unit"] = "B/launch"
@@ -216,16 +216,16 @@ def main():
         dist.destroy_process_group()
 
 
-def _pmc_traffic(label):
+def _pmc_traffic(label, workload):
     """HBM bytes per launch of `label` measured by rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) over
     this same bench, reduced by tools/traffic.py into profiles/traffic.json; None if the committed
-    measurement is for another kernel."""
+    measurement is for another kernel or another workload."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
     try:
         tr = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if tr.get("kernel") != label:
+    if tr.get("kernel") != label or tr.get("workload", "vit_large 16x256^2 B=24") != workload:
         return None
     tr["source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py)"
     return tr

@@ -39,13 +39,14 @@ def per_launch(d, counter, rx):
 
 def main():
     fetch_dir, write_dir, label, out = sys.argv[1:5]
+    workload = sys.argv[5] if len(sys.argv) > 5 else "vit_large 16x256^2 B=24"  # bench.py's default run
     rx = name_regex(label)
     fetch = per_launch(fetch_dir, "FETCH_SIZE", rx)
     write = per_launch(write_dir, "WRITE_SIZE", rx)
     assert fetch and write, f"no launches of {label} ({rx.pattern}) in the PMC passes"
     fkib = sum(fetch) / len(fetch)
     wkib = sum(write) / len(write)
-    res = {"kernel": label, "rocprof_regex": rx.pattern, "launches": [len(fetch), len(write)],
+    res = {"kernel": label, "workload": workload, "rocprof_regex": rx.pattern, "launches": [len(fetch), len(write)],
            "fetch_kib_per_launch": round(fkib, 1), "write_kib_per_launch": round(wkib, 1),
            "hbm_bytes_per_launch": round((2.0 * fkib + wkib) * 1024.0),
            "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (KiB units; gfx950 FETCH_SIZE "

@@ -13,6 +13,8 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short bf16_t;  // storage type of a bf16 element in global memory
 
 #define LDS_AS __attribute__((address_space(3)))
@@ -100,6 +102,15 @@ template <typename T, int N>
 __device__ __forceinline__ void tie(T (&x)[N]) {
 #pragma unroll
   for (int i = 0; i < N; ++i) asm volatile("" : "+v"(x[i]));
+}
+
+// 4 f32 -> 4 fp8 e4m3 (OCP, RNE), clamped to the format's +-448 (e4m3fn has no infinity)
+__device__ __forceinline__ uint32_t f8pack4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(a, -448.f, 448.f),
+                                          __builtin_amdgcn_fmed3f(b, -448.f, 448.f), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(c, -448.f, 448.f),
+                                      __builtin_amdgcn_fmed3f(d, -448.f, 448.f), w, true);
+  return (uint32_t)w;
 }
 
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }

@@ -19,7 +19,7 @@ namespace {
 // LayerNorm forward: wave per row. x f32 or bf16 [M, ldx]; y bf16 or f32 [M, ldy]; optional affine.
 constexpr int LN_MAXV = 8;  // float4 per lane -> D <= 64*4*8 = 2048
 
-template <bool XBF, bool YF32, int NV>
+template <bool XBF, bool YF32, int NV, bool YF8 = false>
 __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __restrict__ x, long ldx,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 float eps, void* __restrict__ y, long ldy, float* __restrict__ mean,
@@ -63,7 +63,9 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
         const float4 b = *(const float4*)(beta + c);
         o[0] = o[0] * g.x + b.x; o[1] = o[1] * g.y + b.y; o[2] = o[2] * g.z + b.z; o[3] = o[3] * g.w + b.w;
       }
-      if constexpr (YF32) {
+      if constexpr (YF8) {  // unscaled e4m3 operand of the fp8 QKV / fc1 GEMMs (|y| <= 448 clamp)
+        *(uint32_t*)((unsigned char*)y + row * ldy + c) = f8pack4(o[0], o[1], o[2], o[3]);
+      } else if constexpr (YF32) {
         *(float4*)((float*)y + row * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
       } else {
         *(uint2*)((bf16_t*)y + row * ldy + c) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
@@ -591,6 +593,86 @@ static int ln_nv(int D) {  // float4 per lane for a row of D floats (templated r
   return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 6 ? 6 : 8;
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// fp8 e4m3 quantisation (the fp8 target-encoder path). amax: max |x| as its f32 bit pattern
+// (non-negative floats order like their bits, so an integer max is exact and order-independent).
+// quant: y = e4m3(x * 2^-e), e = the least exponent with amax * 2^-e <= 448 (0 without amax).
+template <bool XBF>
+__global__ __launch_bounds__(256) void k_amax(long n, const void* __restrict__ x, unsigned* __restrict__ amax) {
+  __shared__ unsigned red[4];
+  unsigned m = 0;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += (long)gridDim.x * 256 * 8) {
+    float v[8];
+    if (i + 8 <= n) {
+      if constexpr (XBF) {
+        const uint4 u = *(const uint4*)((const bf16_t*)x + i);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[2 * j] = bf2f(w[j] & 0xffff); v[2 * j + 1] = bf2f(w[j] >> 16); }
+      } else {
+        const float4 a = *(const float4*)((const float*)x + i), b = *(const float4*)((const float*)x + i + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = i + j < n ? (XBF ? bf2f(((const bf16_t*)x)[i + j]) : ((const float*)x)[i + j]) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(fabsf(v[j])));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(amax, max(max(red[0], red[1]), max(red[2], red[3])));
+}
+
+__device__ __forceinline__ int f8_exp(const unsigned* amax) {
+  if (!amax) return 0;
+  const float a = __uint_as_float(*amax);
+  if (!(a > 0.f) || !(a < 3.0e38f)) return 0;  // zero / non-finite tensor: unscaled
+  int e = (int)ceilf(log2f(a / 448.f));
+  if (ldexpf(a, -e) > 448.f) ++e;
+  if (ldexpf(a, -(e - 1)) <= 448.f) --e;
+  return min(max(e, -100), 100);
+}
+
+template <bool XBF>
+__global__ __launch_bounds__(256) void k_quant_fp8(long n, const void* __restrict__ x, unsigned char* __restrict__ y,
+                                                   const unsigned* __restrict__ amax, int* __restrict__ scale_exp) {
+  const int e = f8_exp(amax);
+  const float s = ldexpf(1.f, -e);
+  if (scale_exp && blockIdx.x == 0 && threadIdx.x == 0) scale_exp[0] = e;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += (long)gridDim.x * 256 * 8) {
+    float v[8];
+    const bool full = i + 8 <= n;
+    if (full) {
+      if constexpr (XBF) {
+        const uint4 u = *(const uint4*)((const bf16_t*)x + i);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[2 * j] = bf2f(w[j] & 0xffff); v[2 * j + 1] = bf2f(w[j] >> 16); }
+      } else {
+        const float4 a = *(const float4*)((const float*)x + i), b = *(const float4*)((const float*)x + i + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = i + j < n ? (XBF ? bf2f(((const bf16_t*)x)[i + j]) : ((const float*)x)[i + j]) : 0.f;
+    }
+    const uint32_t lo = f8pack4(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+    const uint32_t hi = f8pack4(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
+    if (full) {
+      *(uint2*)(y + i) = make_uint2(lo, hi);
+    } else {
+      for (int j = 0; j < 8 && i + j < n; ++j) y[i + j] = (unsigned char)((j < 4 ? lo : hi) >> (8 * (j & 3)));
+    }
+  }
+}
+
 // ================================================================================================
 // C ABI
 extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma,
@@ -605,7 +687,19 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
   const int nv = ln_nv(D);
 #define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, YF, NVV>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
 #define LNF_NV(XB, YF) switch (nv) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 4: LNF(XB, YF, 4); break; case 6: LNF(XB, YF, 6); break; default: LNF(XB, YF, 8); }
-  if (x_bf16 && y_f32) { LNF_NV(true, true) }
+#define LNF8(XB, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, false, NVV, true>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
+  if (y_f32 == 2) {  // fp8 e4m3 output
+    VJ_CHECK_ARG(ldy % 16 == 0 && !((uintptr_t)y & 15), "vj_layernorm_fwd: fp8 output needs 16-B rows");
+    switch (nv) {
+      case 1: if (x_bf16) LNF8(true, 1); else LNF8(false, 1); break;
+      case 2: if (x_bf16) LNF8(true, 2); else LNF8(false, 2); break;
+      case 4: if (x_bf16) LNF8(true, 4); else LNF8(false, 4); break;
+      case 6: if (x_bf16) LNF8(true, 6); else LNF8(false, 6); break;
+      default: if (x_bf16) LNF8(true, 8); else LNF8(false, 8);
+    }
+  }
+#undef LNF8
+  else if (x_bf16 && y_f32) { LNF_NV(true, true) }
   else if (x_bf16) { LNF_NV(true, false) }
   else if (y_f32) { LNF_NV(false, true) }
   else { LNF_NV(false, false) }
@@ -826,5 +920,40 @@ extern "C" int vj_cast_bf16(long n, const float* in, void* out, void* stream) {
   hipLaunchKernelGGL(k_cast_bf16, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4,
                      (const float4*)in, (uint2*)out);
   VJ_LAUNCH_CHECK("vj_cast_bf16");
+  return VJ_OK;
+}
+
+extern "C" int vj_amax(long n, const void* x, int x_bf16, unsigned* amax_bits, void* stream) {
+  VJ_CHECK_ARG(n >= 0 && amax_bits, "vj_amax: bad arguments");
+  VJ_CHECK_ARG(!((uintptr_t)x & 15), "vj_amax: x must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(amax_bits, 0, sizeof(unsigned), st) != hipSuccess) {
+    vj_set_error("vj_amax: hipMemsetAsync failed");
+    return VJ_ERR_LAUNCH;
+  }
+  if (n == 0) return VJ_OK;
+  long blocks = (n + 2047) / 2048;
+  if (blocks > 2048) blocks = 2048;
+  if (x_bf16) hipLaunchKernelGGL(k_amax<true>, dim3(blocks), dim3(256), 0, st, n, x, amax_bits);
+  else hipLaunchKernelGGL(k_amax<false>, dim3(blocks), dim3(256), 0, st, n, x, amax_bits);
+  VJ_LAUNCH_CHECK("vj_amax");
+  return VJ_OK;
+}
+
+extern "C" int vj_quant_fp8(long n, const void* x, int x_bf16, void* y, const unsigned* amax_bits, int* scale_exp,
+                            void* stream) {
+  VJ_CHECK_ARG(n >= 0 && y, "vj_quant_fp8: bad arguments");
+  VJ_CHECK_ARG(!((uintptr_t)x & 15) && !((uintptr_t)y & 7), "vj_quant_fp8: x 16-B / y 8-B aligned");
+  if (n == 0 && !scale_exp) return VJ_OK;
+  long blocks = (n + 2047) / 2048;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipStream_t st = (hipStream_t)stream;
+  if (x_bf16)
+    hipLaunchKernelGGL(k_quant_fp8<true>, dim3(blocks), dim3(256), 0, st, n, x, (unsigned char*)y, amax_bits, scale_exp);
+  else
+    hipLaunchKernelGGL(k_quant_fp8<false>, dim3(blocks), dim3(256), 0, st, n, x, (unsigned char*)y, amax_bits,
+                       scale_exp);
+  VJ_LAUNCH_CHECK("vj_quant_fp8");
   return VJ_OK;
 }

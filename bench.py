@@ -172,10 +172,10 @@ def main():
             roof["traffic_unit"] = "B/launch"
             roof["traffic_source"] = tr["source"]
 
-    # The target encoder's forward runs on a side stream (train.py), so inside the timed region the
-    # dominant kernel shares the CUs with it and its launch durations include that sharing. One more
-    # UNTIMED step with the side stream off gives the same kernel's unshared launch duration.
-    if roof and os.environ.get("VJ_TGT_STREAM", "1") != "0":
+    # With VJ_TGT_STREAM=1 the target encoder's forward runs on a side stream (train.py), so inside
+    # the timed region the dominant kernel shares the CUs with it. One more UNTIMED step with the side
+    # stream off then gives the same kernel's unshared launch duration.
+    if roof and os.environ.get("VJ_TGT_STREAM", "0") == "1":
         solo = ops.KernelEvents(only={dom})
         os.environ["VJ_TGT_STREAM"] = "0"
         torch.cuda.synchronize()
@@ -183,7 +183,7 @@ def main():
         run(nsteps - 1)
         solo.stop()
         torch.cuda.synchronize()
-        del os.environ["VJ_TGT_STREAM"]
+        os.environ["VJ_TGT_STREAM"] = "1"
         st1 = solo.summary()[dom]
         a1 = st1["flops"] / (st1["total_ms"] * 1e-3) / 1e12
         roof["timed_region_shares_cus_with"] = "target-encoder side stream"
@@ -231,12 +231,25 @@ def _pmc_traffic(label, workload):
     return tr
 
 
-def cpu_baseline(args, sample):
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, sample, timed=2):
     """The CPU oracle (fp32, the reference algorithm restated) on a bounded sample: ONE clip of the same
-    workload (ViT-L 16x256^2, the same two masks truncated to B=1), one full step. ~10-30 s."""
+    workload (the same two masks truncated to B=1), one untimed warm-up step, then the median of
+    `timed` full steps (fwd + bwd + AdamW + EMA). Threads: the process's CPU share (OMP_NUM_THREADS on
+    the GPU box = 16; os.cpu_count() there counts the whole machine)."""
     from oracle import vjepa_oracle as orc
 
-    threads = int(os.environ.get("VJ_CPU_THREADS", "16"))
+    threads = int(os.environ.get("VJ_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS") or
+                  len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
     torch.manual_seed(239)
     from vjepa2_amd import vision_transformer as vt
@@ -254,13 +267,18 @@ def cpu_baseline(args, sample):
     clips = sample[0][:1].cpu()
     me = [m[:1].cpu() for m in sample[1]]
     mp = [m[:1].cpu() for m in sample[2]]
-    t0 = time.perf_counter()
-    tr.step(clips, me, mp, 5.25e-4, 0.04, 0.99925)
-    dt = time.perf_counter() - t0
+    tr.step(clips, me, mp, 5.25e-4, 0.04, 0.99925)  # warm-up (allocator, thread pool)
+    times = []
+    for _ in range(timed):
+        t0 = time.perf_counter()
+        tr.step(clips, me, mp, 5.25e-4, 0.04, 0.99925)
+        times.append(time.perf_counter() - t0)
+    dt = sorted(times)[len(times) // 2]
     return {"value": round(1.0 / dt, 4), "unit": "clips/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(),
             "sample": f"1 clip ({args.model} {T}x{S}^2, masks K={[m.shape[1] for m in me]}, "
-                      f"Kp={[m.shape[1] for m in mp]}), one full fp32 step (fwd+bwd+AdamW+EMA) of the CPU oracle, "
-                      f"{dt:.1f} s"}
+                      f"Kp={[m.shape[1] for m in mp]}): one warm-up + median of {timed} full fp32 steps "
+                      f"(fwd+bwd+AdamW+EMA) of the CPU oracle, {dt:.1f} s/step, torch {threads} threads"}
 
 
 if __name__ == "__main__":

@@ -138,6 +138,9 @@ int vj_adamw(long n, float* p, const float* g, float* m, float* v, void* p_bf16,
              float eps, float weight_decay, int step, float grad_scale, const int* found_inf, void* stream);
 int vj_ema(long n, float* target, const float* online, float momentum, void* target_bf16, void* stream);
 int vj_cast_bf16(long n, const float* in, void* out, void* stream);
+/* dst[c][r] = src[r][c] (bf16; rows, cols, strides multiples of 8): the K-major copy W^T that the
+ * data-gradient GEMM dX = dY W (nn.Linear backward) reads as its B operand. */
+int vj_transpose_bf16(int rows, int cols, const void* src, long ld_src, void* dst, long ld_dst, void* stream);
 
 #ifdef __cplusplus
 }

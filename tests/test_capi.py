@@ -30,6 +30,8 @@ def test_library_exports_every_declared_symbol():
     exported = set(re.findall(r"\sT\s(vj_\w+)", out))
     missing = set(declared()) - exported
     assert not missing, f"declared but not exported: {missing}"
+    undeclared = exported - set(declared())
+    assert not undeclared, f"exported but not declared in include/vjepa_hip.h: {undeclared}"
     lib = _lib.load()
     for n in declared():
         getattr(lib, n)

@@ -122,6 +122,8 @@ def test_gemm_epilogues(M, N):
     got2 = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
     ops.gemm(M, K, N, dY, N, True, W2t, N, True, ops.EPI_GELU_BWD, out=got2, ldc=K, aux=pre2, ldaux=K)
     _close(got2, x.grad, 2e-3, 1e-2, "EPI_GELU_BWD (B K-major)")
+    got3 = ops.linear_dgrad(dY, W2, gelu_pre=pre2, wt=ops.transpose_bf16(W2))
+    _close(got3, x.grad, 2e-3, 1e-2, "EPI_GELU_BWD (linear_dgrad on W^T)")
     f32 = torch.empty(M, K, device=DEV)
     ops.gemm(M, K, N, dY, N, True, W2t, N, True, ops.EPI_F32, out=f32, ldc=K)
     _close(f32, dY.float() @ W2.float(), 2e-4 * math.sqrt(N), 1e-5, "EPI_F32 (B K-major)")
@@ -382,6 +384,14 @@ def test_im2col_patch_embed():
     assert cols_all.shape == (B * N, C * tub * p * p)
 
 
+@pytest.mark.parametrize("shape", [(1024, 4096), (1408, 6144), (384, 1152), (72, 200)])
+def test_transpose_bf16(shape):
+    from vjepa2_amd import ops
+
+    x = torch.randn(*shape).to(DEV).bfloat16()
+    assert torch.equal(ops.transpose_bf16(x), x.t().contiguous())
+
+
 def test_row_ops_bit_exact():
     from vjepa2_amd import ops
 
@@ -404,14 +414,25 @@ def test_row_ops_bit_exact():
     assert torch.equal(out, exp)
 
 
-def test_pred_index_matches_argsort():
+@pytest.mark.parametrize("case", ["sorted", "unsorted", "dups", "edge"])
+def test_pred_index_matches_argsort(case):
+    """Merge-path ranks (sorted masks, the collator's output) and the counting fallback (unsorted
+    rows, ids repeated across masks_x / masks_y) both equal the reference's stable torch.argsort
+    (predictor.py:210-217, 240-242)."""
     from vjepa2_amd import ops
 
     g = torch.Generator(device="cpu").manual_seed(3)
     B, N, K, Kp = 4, 2048, 513, 966
+    if case == "edge":
+        K, Kp = 1, 2047
     perms = [torch.randperm(N, generator=g) for _ in range(B)]
     mx = torch.stack([p[:K].sort().values for p in perms])
     my = torch.stack([p[K:K + Kp].sort().values for p in perms])
+    if case == "unsorted":
+        mx[1] = mx[1][torch.randperm(K, generator=g)]
+        my[2] = my[2][torch.randperm(Kp, generator=g)]
+    elif case == "dups":  # masks_y repeats some masks_x ids (still sorted): stability decides the order
+        my = torch.stack([torch.cat([mx[b][:100], my[b][100:]]).sort().values for b in range(B)])
     n = K + Kp
     row0 = 17
     pos = torch.full((row0 + B * n,), -1, dtype=torch.int32, device=DEV)
@@ -420,7 +441,7 @@ def test_pred_index_matches_argsort():
     lrows = torch.empty(B * Kp, dtype=torch.int32, device=DEV)
     ops.pred_index(mx.to(DEV), my.to(DEV), row0, N, pos, ctx, tgt, lrows)
     m = torch.cat([mx, my], 1)
-    order = torch.argsort(m, dim=1)
+    order = torch.argsort(m, dim=1, stable=True)
     sorted_ids = torch.gather(m, 1, order)
     rev = torch.argsort(order, dim=1)
     base = (row0 + torch.arange(B) * n)[:, None]

@@ -1,0 +1,152 @@
+"""GPU: the fused AdamW over flat arenas is torch.optim.AdamW as the reference builds it
+(app/vjepa/utils.py:207-255): same update, same per-parameter step counts (unused mask tokens and
+inf/NaN-skipped steps do not advance), and a state_dict() that interchanges with the reference's
+optimizer state in checkpoints (app/vjepa/train.py:318-329 writes it, app/vjepa/utils.py:121 loads it).
+"""
+
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _models():
+    from vjepa2_amd.predictor import vit_predictor
+    from vjepa2_amd.vision_transformer import VisionTransformer
+    from vjepa2_amd.wrappers import MultiSeqWrapper, PredictorMultiSeqWrapper
+
+    torch.manual_seed(0)
+    enc = VisionTransformer(img_size=32, patch_size=16, num_frames=4, tubelet_size=2, embed_dim=64, depth=2,
+                            num_heads=1, mlp_ratio=4, qkv_bias=True, use_rope=False, uniform_power=True,
+                            norm_layer=lambda d: nn.LayerNorm(d, eps=1e-6))  # pos_embed: a frozen Parameter
+    pred = vit_predictor(img_size=32, use_mask_tokens=True, patch_size=16, num_frames=4, tubelet_size=2,
+                         embed_dim=64, predictor_embed_dim=64, depth=1, num_heads=2, uniform_power=True,
+                         num_mask_tokens=3, use_rope=True)
+    return MultiSeqWrapper(enc), PredictorMultiSeqWrapper(pred)
+
+
+def _ref_opt(encoder, predictor):
+    """app/vjepa/utils.py:224-239 restated: the reference's 4 AdamW param groups."""
+    groups = [
+        {"params": [p for n, p in encoder.named_parameters() if ("bias" not in n) and (len(p.shape) != 1)]},
+        {"params": [p for n, p in predictor.named_parameters() if ("bias" not in n) and (len(p.shape) != 1)]},
+        {"params": [p for n, p in encoder.named_parameters() if ("bias" in n) or (len(p.shape) == 1)],
+         "WD_exclude": True, "weight_decay": 0},
+        {"params": [p for n, p in predictor.named_parameters() if ("bias" in n) or (len(p.shape) == 1)],
+         "WD_exclude": True, "weight_decay": 0},
+    ]
+    return torch.optim.AdamW(groups, betas=(0.9, 0.999), eps=1e-8)
+
+
+def _set_lr_wd(opt, lr, wd):
+    for g in opt.param_groups:
+        g["lr"] = lr
+        if not g.get("WD_exclude", False):
+            g["weight_decay"] = wd
+
+
+def _grads(named, seed, skip=()):
+    g = torch.Generator().manual_seed(seed)
+    return {n: (None if n in skip or not p.requires_grad else torch.randn(p.shape, generator=g))
+            for n, p in named}
+
+
+def test_fused_adamw_matches_torch_and_interchanges_state():
+    from vjepa2_amd.train import init_opt
+
+    enc, pred = _models()
+    enc_ref, pred_ref = copy.deepcopy(enc), copy.deepcopy(pred)
+    enc.to(DEV)
+    pred.to(DEV)
+    opt, _, _, _ = init_opt(enc, pred, iterations_per_epoch=10, start_lr=1e-4, ref_lr=1e-4, warmup=0, num_epochs=1,
+                            mixed_precision=True)
+    ref = _ref_opt(enc_ref, pred_ref)
+    named = list(enc.named_parameters()) + [("p." + n, p) for n, p in pred.named_parameters()]
+    named_ref = dict(list(enc_ref.named_parameters()) + [("p." + n, p) for n, p in pred_ref.named_parameters()])
+    unused = {"p.backbone.mask_tokens.1", "p.backbone.mask_tokens.2"}  # grad None in the reference
+    tokens = [pred.backbone.mask_tokens[1], pred.backbone.mask_tokens[2]]
+    for step, (lr, wd) in enumerate([(5e-4, 0.04), (4e-4, 0.05), (3e-4, 0.06)]):
+        grads = _grads(named, 100 + step, skip=unused)
+        for n, p in named:
+            if grads[n] is not None:
+                p.grad.copy_(grads[n])
+            named_ref[n].grad = grads[n]
+        _set_lr_wd(opt, lr, wd)
+        _set_lr_wd(ref, lr, wd)
+        opt.step(exclude=tokens)
+        ref.step()
+        opt.zero_grad()
+    torch.cuda.synchronize()
+    for n, p in named:
+        torch.testing.assert_close(p.detach().cpu(), named_ref[n].detach(), rtol=2e-6, atol=2e-7, msg=n)
+    # state_dict: same numbering, keys, step counts and moments as torch's
+    sd, sr = opt.state_dict(), ref.state_dict()
+    assert [len(g["params"]) for g in sd["param_groups"]] == [len(g["params"]) for g in sr["param_groups"]]
+    assert [g["params"] for g in sd["param_groups"]] == [g["params"] for g in sr["param_groups"]]
+    assert sorted(sd["state"]) == sorted(sr["state"]), "state for the same parameters (none for unused ones)"
+    for k in sr["state"]:
+        assert float(sd["state"][k]["step"]) == float(sr["state"][k]["step"])
+        for m in ("exp_avg", "exp_avg_sq"):
+            # fp32 elementwise math in a different op order (lerp / fma): ~1 ulp of the O(1) moments
+            torch.testing.assert_close(sd["state"][k][m], sr["state"][k][m], rtol=1e-5, atol=1e-6)
+    for gd, gr in zip(sd["param_groups"], sr["param_groups"]):
+        for key in gr:
+            if key != "params":
+                assert gd[key] == gr[key], (key, gd[key], gr[key])
+    # ours -> torch.optim.AdamW (what the reference's load_checkpoint does) and torch -> ours
+    ref2 = _ref_opt(copy.deepcopy(enc_ref), copy.deepcopy(pred_ref))
+    ref2.load_state_dict(sd)
+    enc2, pred2 = _models()
+    enc2.to(DEV)
+    pred2.to(DEV)
+    opt2, _, _, _ = init_opt(enc2, pred2, iterations_per_epoch=10, start_lr=1e-4, ref_lr=1e-4, warmup=0,
+                             num_epochs=1, mixed_precision=True)
+    opt2.load_state_dict(sr)
+    sd2 = opt2.state_dict()
+    for k in sr["state"]:
+        torch.testing.assert_close(sd2["state"][k]["exp_avg"], sr["state"][k]["exp_avg"], rtol=0, atol=0)
+        assert float(sd2["state"][k]["step"]) == float(sr["state"][k]["step"])
+
+
+def test_inf_skip_does_not_advance_step():
+    """GradScaler.step skips optimizer.step on inf/NaN (train.py:446-451): nothing moves and the
+    bias correction of the next step uses the un-advanced count."""
+    from vjepa2_amd.train import init_opt
+
+    enc, pred = _models()
+    enc_ref, pred_ref = copy.deepcopy(enc), copy.deepcopy(pred)
+    enc.to(DEV)
+    pred.to(DEV)
+    opt, _, _, _ = init_opt(enc, pred, iterations_per_epoch=10, start_lr=1e-4, ref_lr=1e-4, warmup=0, num_epochs=1,
+                            mixed_precision=True)
+    ref = _ref_opt(enc_ref, pred_ref)
+    named = list(enc.named_parameters()) + [("p." + n, p) for n, p in pred.named_parameters()]
+    named_ref = dict(list(enc_ref.named_parameters()) + [("p." + n, p) for n, p in pred_ref.named_parameters()])
+    for step in range(3):
+        grads = _grads(named, 7 + step)
+        if step == 1:  # an inf in one gradient: the whole step is skipped
+            first = next(n for n in grads if grads[n] is not None)
+            grads[first][0] = float("inf")
+        for n, p in named:
+            if grads[n] is not None:
+                p.grad.copy_(grads[n])
+            named_ref[n].grad = grads[n]
+        _set_lr_wd(opt, 5e-4, 0.04)
+        _set_lr_wd(ref, 5e-4, 0.04)
+        before = [a.data.clone() for a in opt.arenas]
+        opt.step(found_inf=opt.check_finite())
+        if step != 1:
+            ref.step()  # the reference's scaler.step() skips it on inf
+        else:
+            torch.cuda.synchronize()
+            assert all(torch.equal(b, a.data) for b, a in zip(before, opt.arenas))
+        opt.zero_grad()
+    torch.cuda.synchronize()
+    assert opt.steps == [2, 2, 2, 2]
+    for n, p in named:
+        torch.testing.assert_close(p.detach().cpu(), named_ref[n].detach(), rtol=2e-6, atol=2e-7, msg=n)

@@ -23,7 +23,9 @@ HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def load(path):
     lib = ctypes.CDLL(path)
     for name, args in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # an older build (A/B against a previous source tree)
+            continue
         fn.argtypes = args
         fn.restype = ctypes.c_int
     return lib
@@ -37,6 +39,13 @@ GEMMS = [
     ("fc1  ctx", 11712, 4096, 1024, 1, 1, 3, 1),
     ("fc2  ctx", 11712, 1024, 4096, 1, 1, 2, 1),
     ("fc1  tgt", 49152, 4096, 1024, 1, 1, 3, 1),
+    ("qkv  tgt", 49152, 3072, 1024, 1, 1, 0, 1),
+    ("proj tgt", 49152, 1024, 1024, 1, 1, 2, 1),
+    ("fc2  tgt", 49152, 1024, 4096, 1, 1, 2, 1),
+    ("fc2  tgt bf16", 49152, 1024, 4096, 1, 1, 0, 1),
+    ("dgrad fc2 Wt", 11712, 4096, 1024, 1, 1, 0, 1),
+    ("dgrad fc2 GELU_BWD Wt", 11712, 4096, 1024, 1, 1, 4, 1),
+    ("pred dgrad fc2 GELU_BWD Wt", 71232, 1536, 384, 1, 1, 4, 1),
     ("dgrad fc2", 11712, 4096, 1024, 1, 0, 0, 1),
     ("dgrad fc1", 11712, 1024, 4096, 1, 0, 0, 1),
     ("dgrad fc2 GELU_BWD", 11712, 4096, 1024, 1, 0, 4, 1),

@@ -10,13 +10,25 @@ Layout choices (HBM, 288 GB per GPU): params ordered by backward readiness (last
 all-reduce buckets are contiguous slices that fill in order; every param padded to 8 elements so
 every view is 16-B aligned for the bf16 DMA loads; weight-decay and no-decay params in separate
 arenas (the reference's 4 AdamW param groups, app/vjepa/utils.py:224-237).
+
+The optimizer's state_dict() is numbered exactly like torch.optim.AdamW's over the reference's
+param groups (app/vjepa/utils.py:224-238: named_parameters() order per group, frozen parameters
+included, no state for parameters that never received a gradient), so checkpoints interchange
+with the reference's `opt` entry (app/vjepa/train.py:318-329, app/vjepa/utils.py:121).
 """
 
+import numpy as np
 import torch
 
 from . import ops
+from .functions import SHADOW_EPOCH
 
 ALIGN = 8
+
+# torch.optim.AdamW param-group defaults (torch 2.10), written into state_dict() groups so a
+# torch.optim.AdamW built like the reference's init_opt loads them unchanged
+_TORCH_ADAMW_KEYS = dict(amsgrad=False, maximize=False, foreach=None, capturable=False, differentiable=False,
+                         fused=None, decoupled_weight_decay=True)
 
 
 def wd_split(named_params):
@@ -32,6 +44,10 @@ def readiness_order(named_params):
     return list(reversed(list(named_params)))
 
 
+def _padded(n):
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
 class FlatArena:
     def __init__(self, named_params, device, grads=True, opt_state=True, name=""):
         self.name = name
@@ -41,7 +57,7 @@ class FlatArena:
         off = 0
         for p in self.params:
             self.offsets.append(off)
-            off += (p.numel() + ALIGN - 1) // ALIGN * ALIGN
+            off += _padded(p.numel())
         self.numel = max(off, ALIGN)
         f32 = dict(dtype=torch.float32, device=device)
         self.data = torch.zeros(self.numel, **f32)
@@ -62,23 +78,18 @@ class FlatArena:
     def sync_bf16(self):
         """Refresh the bf16 shadow after the fp32 params were changed outside the fused kernels."""
         ops.cast_bf16(self.data, out=self.bf16)
+        SHADOW_EPOCH[0] += 1
+
+    def index(self, p):
+        return next(i for i, q in enumerate(self.params) if q is p)
 
     def segment(self, p):
-        i = next(i for i, q in enumerate(self.params) if q is p)
+        i = self.index(p)
         return self.offsets[i], self.params[i].numel()
 
-    def ranges(self, exclude=()):
-        """Contiguous [lo, hi) ranges covering the arena minus the segments of `exclude` params."""
-        ex = sorted((self.segment(p)[0], self.segment(p)[0] + (p.numel() + ALIGN - 1) // ALIGN * ALIGN)
-                    for p in exclude if any(p is q for q in self.params))
-        out, lo = [], 0
-        for a, b in ex:
-            if a > lo:
-                out.append((lo, a))
-            lo = b
-        if lo < self.numel:
-            out.append((lo, self.numel))
-        return out
+    def span(self, i, j):
+        """[lo, hi) of params i .. j-1 (contiguous, padding included)."""
+        return self.offsets[i], self.offsets[j - 1] + _padded(self.params[j - 1].numel())
 
     def zero_grad(self):
         if self.grad is not None:
@@ -86,25 +97,85 @@ class FlatArena:
 
 
 class FusedAdamW:
-    """torch.optim.AdamW semantics (decoupled weight decay, bias correction) over arenas, one kernel
-    launch per arena (the four param groups of app/vjepa/utils.py:207-255), bf16 shadow written in
-    the same pass. `param_groups` mirrors torch's so the LR / WD schedulers drive it."""
+    """torch.optim.AdamW semantics (decoupled weight decay, bias correction) over arenas: one kernel
+    launch per run of parameters with equal step count (normally one per arena = one per param
+    group of app/vjepa/utils.py:207-255), bf16 shadow written in the same pass. `param_groups`
+    mirrors torch's so the LR / WD schedulers drive it.
 
-    def __init__(self, arenas, wd_exclude, betas=(0.9, 0.999), eps=1e-8, lr=1e-3, weight_decay=1e-2):
+    Step counts are per parameter, as in torch: a parameter excluded from a step (an unused mask
+    token, whose grad is None in the reference) does not advance, and a step skipped for an inf/NaN
+    gradient (GradScaler.step, train.py:446-451) advances nothing. The skip is decided on the device
+    (no host sync in the step); the host learns it lazily from a pinned copy of the flag at the next
+    step() / state_dict()."""
+
+    def __init__(self, arenas, wd_exclude, betas=(0.9, 0.999), eps=1e-8, lr=1e-3, weight_decay=1e-2,
+                 ref_groups=None):
         self.arenas = arenas
-        self.param_groups = [dict(lr=lr, weight_decay=0.0 if ex else weight_decay, WD_exclude=ex, betas=tuple(betas),
-                                  eps=eps, params=a.params) for a, ex in zip(arenas, wd_exclude)]
-        self.steps = [0] * len(arenas)
+        self.param_groups = []
+        for a, ex in zip(arenas, wd_exclude):  # ex: None (no key: decayed group) or the WD_exclude flag
+            g = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay if ex is None else 0.0,
+                     **_TORCH_ADAMW_KEYS)
+            if ex is not None:
+                g["WD_exclude"] = bool(ex)
+            g["params"] = a.params
+            self.param_groups.append(g)
+        # the reference's per-group parameter lists (named_parameters order, frozen params included)
+        self.ref_groups = ref_groups if ref_groups is not None else [readiness_order(zip(a.names, a.params))
+                                                                     for a in arenas]
+        self.where = {}
+        for i, a in enumerate(arenas):
+            for j, p in enumerate(a.params):
+                self.where[id(p)] = (i, j)
+        self.pstep = [np.zeros(len(a.params), dtype=np.int64) for a in arenas]
         self.found_inf = None
+        self._pending = None  # (pinned flag copy, event, [(arena, param indices advanced)])
+
+    @property
+    def steps(self):
+        """Per-arena step count (of its first parameter; all equal unless some were excluded)."""
+        self._resolve()
+        return [int(s.max()) if len(s) else 0 for s in self.pstep]
+
+    def _resolve(self):
+        if self._pending is None:
+            return
+        flag, ev, advanced = self._pending
+        ev.synchronize()
+        if int(flag[0]) != 0:  # that step was skipped on the device
+            for i, idx in advanced:
+                self.pstep[i][idx] -= 1
+        self._pending = None
 
     def step(self, grad_scale=1.0, found_inf=None, exclude=()):
+        self._resolve()
+        ex = {id(p) for p in exclude}
+        advanced = []
         for i, (g, a) in enumerate(zip(self.param_groups, self.arenas)):
-            self.steps[i] += 1
+            act = np.array([id(p) not in ex for p in a.params], dtype=bool)
+            st = self.pstep[i]
+            st[act] += 1
+            advanced.append((i, np.nonzero(act)[0]))
             b1, b2 = g["betas"]
-            wd = 0.0 if g["WD_exclude"] else g["weight_decay"]
-            for lo, hi in a.ranges(exclude):
+            wd = 0.0 if g.get("WD_exclude", False) else g["weight_decay"]
+            j, n = 0, len(a.params)
+            while j < n:  # maximal runs of active params with equal step count
+                if not act[j]:
+                    j += 1
+                    continue
+                k = j + 1
+                while k < n and act[k] and st[k] == st[j]:
+                    k += 1
+                lo, hi = a.span(j, k)
                 ops.adamw(a.data[lo:hi], a.grad[lo:hi], a.exp_avg[lo:hi], a.exp_avg_sq[lo:hi], a.bf16[lo:hi], g["lr"],
-                          b1, b2, g["eps"], wd, self.steps[i], grad_scale=grad_scale, found_inf=found_inf)
+                          b1, b2, g["eps"], wd, int(st[j]), grad_scale=grad_scale, found_inf=found_inf)
+                j = k
+        SHADOW_EPOCH[0] += 1  # the bf16 shadows changed: cached W^T copies are stale
+        if found_inf is not None:
+            flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            flag.copy_(found_inf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending = (flag, ev, advanced)
 
     def zero_grad(self, set_to_none=False):
         for a in self.arenas:
@@ -120,39 +191,64 @@ class FusedAdamW:
         return self.found_inf
 
     def state_dict(self):
-        """torch.optim.AdamW-style state (param index order = arena order within each group)."""
+        """torch.optim.AdamW.state_dict() of the reference's optimizer (app/vjepa/utils.py:224-239):
+        parameters numbered across the 4 groups in named_parameters() order; state only for
+        parameters that have taken a step."""
+        self._resolve()
         state, groups, idx = {}, [], 0
-        for i, (g, a) in enumerate(zip(self.param_groups, self.arenas)):
+        for g, refs in zip(self.param_groups, self.ref_groups):
             ids = []
-            for p, o in zip(a.params, a.offsets):
-                n = p.numel()
-                state[idx] = dict(step=torch.tensor(float(self.steps[i])),
-                                  exp_avg=a.exp_avg[o:o + n].view(p.shape).clone(),
-                                  exp_avg_sq=a.exp_avg_sq[o:o + n].view(p.shape).clone())
+            for _, p in refs:
+                loc = self.where.get(id(p))
+                if loc is not None and self.pstep[loc[0]][loc[1]] > 0:
+                    i, j = loc
+                    a = self.arenas[i]
+                    o, n = a.offsets[j], p.numel()
+                    state[idx] = dict(step=torch.tensor(float(self.pstep[i][j])),
+                                      exp_avg=a.exp_avg[o:o + n].view(p.shape).detach().cpu().clone(),
+                                      exp_avg_sq=a.exp_avg_sq[o:o + n].view(p.shape).detach().cpu().clone())
                 ids.append(idx)
                 idx += 1
-            groups.append({k: v for k, v in g.items() if k != "params"} | dict(params=ids))
+            sg = {k: v for k, v in g.items() if k != "params"}
+            sg["params"] = ids
+            groups.append(sg)
         return dict(state=state, param_groups=groups)
 
     def load_state_dict(self, sd):
-        idx = 0
-        for i, (g, a) in enumerate(zip(self.param_groups, self.arenas)):
-            sg = sd["param_groups"][i]
+        """Accepts the reference's torch.optim.AdamW state (or ours): state entries are matched to
+        parameters by their index in the reference numbering."""
+        self._resolve()
+        if len(sd["param_groups"]) != len(self.param_groups):
+            raise ValueError(f"optimizer state has {len(sd['param_groups'])} param groups, expected "
+                             f"{len(self.param_groups)}")
+        for g, refs, sg in zip(self.param_groups, self.ref_groups, sd["param_groups"]):
+            if len(sg["params"]) != len(refs):
+                raise ValueError(f"param group of {len(sg['params'])} params in the state, {len(refs)} in the model")
             for k in ("lr", "weight_decay", "betas", "eps"):
                 if k in sg:
                     g[k] = tuple(sg[k]) if k == "betas" else sg[k]
-            for p, o in zip(a.params, a.offsets):
-                st = sd["state"].get(idx, sd["state"].get(str(idx)))
-                idx += 1
-                if not st:
+            for pid, (pname, p) in zip(sg["params"], refs):
+                loc = self.where.get(id(p))
+                st = sd["state"].get(pid, sd["state"].get(str(pid)))
+                if loc is None:
                     continue
-                n = p.numel()
+                i, j = loc
+                a = self.arenas[i]
+                o, n = a.offsets[j], p.numel()
+                if not st:
+                    self.pstep[i][j] = 0
+                    a.exp_avg[o:o + n].zero_()
+                    a.exp_avg_sq[o:o + n].zero_()
+                    continue
+                if st["exp_avg"].numel() != n:
+                    raise ValueError(f"state of {pname}: {st['exp_avg'].numel()} elements, parameter has {n}")
                 a.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
                 a.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
-                self.steps[i] = int(float(st["step"]))
+                self.pstep[i][j] = int(float(st["step"]))
 
 
 def fused_ema(target_arenas, online_arenas, momentum):
     """train.py:456-465: target = target * m + (1 - m) * online, per arena, bf16 shadow refreshed."""
     for t, o in zip(target_arenas, online_arenas):
         ops.ema(t.data, o.data, momentum, t.bf16)
+    SHADOW_EPOCH[0] += 1

@@ -121,3 +121,37 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 }
 
 static inline int vj_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// erf with |abs err| <= 1.5e-7 (Abramowitz-Stegun 7.1.26): far below the bf16 rounding of the output.
+__device__ __forceinline__ float erf_fast(float z) {
+  const float a = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float r = 1.f - p * __expf(-a * a);
+  return copysignf(r, z);
+}
+// nn.GELU() (exact erf form, vision_transformer.py:100) and its derivative
+__device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+  return 0.5f * (1.f + erf_fast(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
+
+// 3-axis RoPE applied to the q and k columns of a fused QKV projection (modules.py:26-50, 343-365),
+// as a GEMM epilogue argument
+struct VjRope {
+  const int* ids;   // token id per row (NULL -> row % mod)
+  int mod, tpf, tpr;
+  int half, hd, D;  // half = slice/2, head dim, q/k block width (= H * hd)
+  const float* cos_t;
+  const float* sin_t;
+  int npos;         // table rows (positions); every position of every id is < npos
+};
+
+__device__ __forceinline__ uint32_t clamp_u31(long b) {
+  if (b < 0) return 0;
+  return b > 0x7fffffffL ? 0x7fffffffu : (uint32_t)b;
+}

@@ -360,22 +360,59 @@ __global__ void k_add_rows(int R, int D, float* __restrict__ dst, long ldd, cons
 //   ctx_dst[b*K + i]            = row0 + b*n + rank(i)        (where context token i goes)
 //   tgt_rows[b*Kp + j]          = row0 + b*n + rank(K + j)    (where target token j sits)
 //   loss_rows[b*Kp + j]         = (b % bmod)*N + my[b][j]     (row of the target-encoder output)
-// One block per b; ids staged in LDS; O(n^2) compares (n <= ~8k).
+// One block per b, ids staged in LDS. The collator's masks are sorted ascending per row
+// (multiseq_multiblock3d.py:201-202, argwhere / nonzero), so the rank is a merge-path position:
+// rank(mx[i]) = i + #{my < mx[i]}, rank(my[j]) = j + #{mx <= my[j]} (binary searches in LDS, the
+// <= keeps argsort's stability: equal ids of masks_x come first). Rows that are not sorted fall back
+// to counting ranks over the whole row (O(n^2), same result).
+__device__ __forceinline__ int lower_bound_lds(const int* a, int n, int v) {  // #{a < v}
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int upper_bound_lds(const int* a, int n, int v) {  // #{a <= v}
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
 __global__ void k_pred_index(int K, int Kp, const long* __restrict__ mx, const long* __restrict__ my, int row0,
                              int bmod, int N, int* __restrict__ pos, int* __restrict__ ctx_dst,
                              int* __restrict__ tgt_rows, int* __restrict__ loss_rows) {
   extern __shared__ int ids[];
+  __shared__ int unsorted;
   const int b = blockIdx.x;
   const int n = K + Kp;
+  if (threadIdx.x == 0) unsorted = 0;
+  __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x)
     ids[i] = (int)(i < K ? mx[(long)b * K + i] : my[(long)b * Kp + (i - K)]);
   __syncthreads();
+  bool bad = false;
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    if (i + 1 < n && i + 1 != K && ids[i + 1] < ids[i]) bad = true;
+  if (bad) unsorted = 1;
+  __syncthreads();
+  const bool sorted = unsorted == 0;
+  const int* xs = ids;
+  const int* ys = ids + K;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int v = ids[i];
     int rank = 0;
-    for (int j = 0; j < n; ++j) {
-      const int w = ids[j];
-      rank += (w < v) || (w == v && j < i);
+    if (sorted) {
+      rank = i < K ? i + lower_bound_lds(ys, Kp, v) : (i - K) + upper_bound_lds(xs, K, v);
+    } else {
+      for (int j = 0; j < n; ++j) {
+        const int w = ids[j];
+        rank += (w < v) || (w == v && j < i);
+      }
     }
     const int dst = row0 + b * n + rank;
     pos[dst] = v;
@@ -581,6 +618,39 @@ __global__ void k_cast_bf16(long n4, const float4* __restrict__ in, uint2* __res
   }
 }
 
+// bf16 transpose dst[c][r] = src[r][c] through a 64 x 64 LDS tile (16-B loads and stores): the
+// K-major copy W^T of a weight that the data-gradient GEMM dX = dY W reads (direct-store epilogue).
+__global__ __launch_bounds__(256) void k_transpose_bf16(int rows, int cols, const bf16_t* __restrict__ src, long lds_,
+                                                        bf16_t* __restrict__ dst, long ldd) {
+  __shared__ bf16_t t[64][64 + 2];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tr = threadIdx.x >> 3, tc = (threadIdx.x & 7) * 8;  // 32 rows x 8 chunks of 8 per pass
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int r = r0 + tr + 32 * p, c = c0 + tc;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < rows && c < cols) v = *(const uint4*)(src + (long)r * lds_ + c);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      t[tr + 32 * p][tc + 2 * k] = (bf16_t)(w[k] & 0xffff);
+      t[tr + 32 * p][tc + 2 * k + 1] = (bf16_t)(w[k] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int c = c0 + tr + 32 * p, r = r0 + tc;  // output row c, columns r .. r+7
+    if (c < cols && r < rows) {
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        w[k] = (uint32_t)t[tc + 2 * k][tr + 32 * p] | ((uint32_t)t[tc + 2 * k + 1][tr + 32 * p] << 16);
+      *(uint4*)(dst + (long)c * ldd + r) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
 inline int grid_stride_blocks(long n4) {
   long b = (n4 + 255) / 256;
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
@@ -593,88 +663,6 @@ static int ln_nv(int D) {  // float4 per lane for a row of D floats (templated r
   return v <= 1 ? 1 : v <= 2 ? 2 : v <= 4 ? 4 : v <= 6 ? 6 : 8;
 }
 
-
-// ------------------------------------------------------------------------------------------------
-// fp8 e4m3 quantisation (the fp8 target-encoder path). amax: max |x| as its f32 bit pattern
-// (non-negative floats order like their bits, so an integer max is exact and order-independent).
-// quant: y = e4m3(x * 2^-e), e = the least exponent with amax * 2^-e <= 448 (0 without amax).
-template <bool XBF>
-__global__ __launch_bounds__(256) void k_amax(long n, const void* __restrict__ x, unsigned* __restrict__ amax) {
-  __shared__ unsigned red[4];
-  unsigned m = 0;
-  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += (long)gridDim.x * 256 * 8) {
-    float v[8];
-    if (i + 8 <= n) {
-      if constexpr (XBF) {
-        const uint4 u = *(const uint4*)((const bf16_t*)x + i);
-        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { v[2 * j] = bf2f(w[j] & 0xffff); v[2 * j + 1] = bf2f(w[j] >> 16); }
-      } else {
-        const float4 a = *(const float4*)((const float*)x + i), b = *(const float4*)((const float*)x + i + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = i + j < n ? (XBF ? bf2f(((const bf16_t*)x)[i + j]) : ((const float*)x)[i + j]) : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(fabsf(v[j])));
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) atomicMax(amax, max(max(red[0], red[1]), max(red[2], red[3])));
-}
-
-__device__ __forceinline__ int f8_exp(const unsigned* amax) {
-  if (!amax) return 0;
-  const float a = __uint_as_float(*amax);
-  if (!(a > 0.f) || !(a < 3.0e38f)) return 0;  // zero / non-finite tensor: unscaled
-  int e = (int)ceilf(log2f(a / 448.f));
-  if (ldexpf(a, -e) > 448.f) ++e;
-  if (ldexpf(a, -(e - 1)) <= 448.f) --e;
-  return min(max(e, -100), 100);
-}
-
-template <bool XBF>
-__global__ __launch_bounds__(256) void k_quant_fp8(long n, const void* __restrict__ x, unsigned char* __restrict__ y,
-                                                   const unsigned* __restrict__ amax, int* __restrict__ scale_exp) {
-  const int e = f8_exp(amax);
-  const float s = ldexpf(1.f, -e);
-  if (scale_exp && blockIdx.x == 0 && threadIdx.x == 0) scale_exp[0] = e;
-  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += (long)gridDim.x * 256 * 8) {
-    float v[8];
-    const bool full = i + 8 <= n;
-    if (full) {
-      if constexpr (XBF) {
-        const uint4 u = *(const uint4*)((const bf16_t*)x + i);
-        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { v[2 * j] = bf2f(w[j] & 0xffff); v[2 * j + 1] = bf2f(w[j] >> 16); }
-      } else {
-        const float4 a = *(const float4*)((const float*)x + i), b = *(const float4*)((const float*)x + i + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = i + j < n ? (XBF ? bf2f(((const bf16_t*)x)[i + j]) : ((const float*)x)[i + j]) : 0.f;
-    }
-    const uint32_t lo = f8pack4(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
-    const uint32_t hi = f8pack4(v[4] * s, v[5] * s, v[6] * s, v[7] * s);
-    if (full) {
-      *(uint2*)(y + i) = make_uint2(lo, hi);
-    } else {
-      for (int j = 0; j < 8 && i + j < n; ++j) y[i + j] = (unsigned char)((j < 4 ? lo : hi) >> (8 * (j & 3)));
-    }
-  }
-}
-
-// ================================================================================================
-// C ABI
 extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma,
                                 const float* beta, float eps, void* y, int y_f32, long ldy, float* mean, float* rstd,
                                 void* stream) {
@@ -923,37 +911,16 @@ extern "C" int vj_cast_bf16(long n, const float* in, void* out, void* stream) {
   return VJ_OK;
 }
 
-extern "C" int vj_amax(long n, const void* x, int x_bf16, unsigned* amax_bits, void* stream) {
-  VJ_CHECK_ARG(n >= 0 && amax_bits, "vj_amax: bad arguments");
-  VJ_CHECK_ARG(!((uintptr_t)x & 15), "vj_amax: x must be 16-B aligned");
-  hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(amax_bits, 0, sizeof(unsigned), st) != hipSuccess) {
-    vj_set_error("vj_amax: hipMemsetAsync failed");
-    return VJ_ERR_LAUNCH;
-  }
-  if (n == 0) return VJ_OK;
-  long blocks = (n + 2047) / 2048;
-  if (blocks > 2048) blocks = 2048;
-  if (x_bf16) hipLaunchKernelGGL(k_amax<true>, dim3(blocks), dim3(256), 0, st, n, x, amax_bits);
-  else hipLaunchKernelGGL(k_amax<false>, dim3(blocks), dim3(256), 0, st, n, x, amax_bits);
-  VJ_LAUNCH_CHECK("vj_amax");
-  return VJ_OK;
-}
-
-extern "C" int vj_quant_fp8(long n, const void* x, int x_bf16, void* y, const unsigned* amax_bits, int* scale_exp,
-                            void* stream) {
-  VJ_CHECK_ARG(n >= 0 && y, "vj_quant_fp8: bad arguments");
-  VJ_CHECK_ARG(!((uintptr_t)x & 15) && !((uintptr_t)y & 7), "vj_quant_fp8: x 16-B / y 8-B aligned");
-  if (n == 0 && !scale_exp) return VJ_OK;
-  long blocks = (n + 2047) / 2048;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  hipStream_t st = (hipStream_t)stream;
-  if (x_bf16)
-    hipLaunchKernelGGL(k_quant_fp8<true>, dim3(blocks), dim3(256), 0, st, n, x, (unsigned char*)y, amax_bits, scale_exp);
-  else
-    hipLaunchKernelGGL(k_quant_fp8<false>, dim3(blocks), dim3(256), 0, st, n, x, (unsigned char*)y, amax_bits,
-                       scale_exp);
-  VJ_LAUNCH_CHECK("vj_quant_fp8");
+extern "C" int vj_transpose_bf16(int rows, int cols, const void* src, long ld_src, void* dst, long ld_dst,
+                                 void* stream) {
+  if (rows == 0 || cols == 0) return VJ_OK;
+  VJ_CHECK_ARG(rows > 0 && cols > 0 && src && dst, "vj_transpose_bf16: bad arguments");
+  VJ_CHECK_ARG(rows % 8 == 0 && cols % 8 == 0 && ld_src % 8 == 0 && ld_dst % 8 == 0 && ld_src >= cols &&
+                   ld_dst >= rows && !(((uintptr_t)src | (uintptr_t)dst) & 15),
+               "vj_transpose_bf16: rows, cols, strides must be multiples of 8 and the pointers 16-B aligned");
+  const dim3 grid(vj_cdiv(cols, 64), vj_cdiv(rows, 64));
+  hipLaunchKernelGGL(k_transpose_bf16, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const bf16_t*)src,
+                     ld_src, (bf16_t*)dst, ld_dst);
+  VJ_LAUNCH_CHECK("vj_transpose_bf16");
   return VJ_OK;
 }

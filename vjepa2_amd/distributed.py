@@ -34,17 +34,20 @@ def init_distributed(port=37129, rank_and_world_size=(None, None), backend=None)
             return 1, 0
     if world == 1:
         return 1, 0
+    os.environ.setdefault("MASTER_PORT", str(port))
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl" and torch.cuda.is_available():
+        # the caller has bound this rank's GPU (torch.cuda.set_device(LOCAL_RANK)); RCCL connects
+        # eagerly on it, so binding afterwards would put every rank on the same device
+        kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
     try:
-        os.environ.setdefault("MASTER_PORT", str(port))
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        kw = {}
-        if backend == "nccl" and torch.cuda.is_available():
-            kw["device_id"] = torch.device("cuda", torch.cuda.current_device())
         dist.init_process_group(backend=backend, world_size=world, rank=rank, **kw)
-    except Exception as e:  # reference behaviour: fall back to a single process
-        logger.info(f"distributed training not available: {e}")
-        return 1, 0
+    except Exception as e:
+        # The reference falls back to a single process here (distributed.py:47-49). With a world
+        # size > 1 explicitly requested that silently trains unsynchronised replicas, so raise.
+        raise RuntimeError(f"init_process_group({backend}, world={world}, rank={rank}) failed: {e}") from e
     return world, rank
 
 

@@ -33,6 +33,24 @@ def weight_bf16(p):
     return c[1]
 
 
+# Bumped whenever the arenas' bf16 shadows are rewritten (AdamW, EMA, sync): invalidates W^T copies.
+SHADOW_EPOCH = [0]
+
+
+def weight_bf16_t(p):
+    """W^T [in, out] bf16 contiguous: the K-major B operand of the data-gradient GEMM dX = dY W
+    (ops.linear_dgrad). Transposed by a HIP kernel once per weight update and cached."""
+    src = weight_bf16(p)
+    arena_owned = getattr(p, "_vj_bf16", None) is not None
+    key = (src.data_ptr(), SHADOW_EPOCH[0] if arena_owned else p._version)
+    c = getattr(p, "_vj_bf16_t", None)
+    if c is None or c[0] != key:
+        out = c[1] if c is not None and c[1].shape == (src.shape[1], src.shape[0]) else None
+        c = (key, ops.transpose_bf16(src.reshape(src.shape[0], -1), out=out))
+        p._vj_bf16_t = c
+    return c[1]
+
+
 def grad_buf(p):
     if p.grad is None:
         p.grad = torch.zeros_like(p)
@@ -128,23 +146,23 @@ def block_backward(dxo, blk, lay, saved):
     twin = getattr(dxo, "_vj_grad_bf16", None)  # bf16 twin written by the next block's LN1 backward,
     dxo_b = twin[0] if twin is not None and twin[1] == dxo._version else ops.cast_bf16(dxo)  # unless changed since
     # MLP
-    dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_pre=pre)
+    dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_pre=pre, wt=weight_bf16_t(mlp.fc2.weight))
     ops.linear_wgrad(dxo_b, act, grad_buf(mlp.fc2.weight))  # fc2 bias grad: fused into LN2 backward
-    dln2 = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight))
+    dln2 = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
     ops.linear_wgrad(dpre, ln2, grad_buf(mlp.fc1.weight))
     _bias_grad(mlp.fc1, dpre)
     gw, gb = _ln_grads(blk.norm2)
     dxm, dxm_b = ops.layernorm_bwd(dln2, x_mid, m2, r2, blk.norm2.weight, dres_in=dxo, dweight=gw, dbias=gb,
                                    want_bf16=True, sum_in=_bias_buf(mlp.fc2), sum_out=_bias_buf(attn.proj))
     # attention (proj bias grad = column sums of dxm, produced above)
-    do = ops.linear_dgrad(dxm_b, weight_bf16(attn.proj.weight))
+    do = ops.linear_dgrad(dxm_b, weight_bf16(attn.proj.weight), wt=weight_bf16_t(attn.proj.weight))
     ops.linear_wgrad(dxm_b, o, grad_buf(attn.proj.weight))
     rope = None
     if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
     dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope)
-    dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight))
+    dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
     ops.linear_wgrad(dqkv, ln1, grad_buf(attn.qkv.weight))
     _bias_grad(attn.qkv, dqkv)
     gw, gb = _ln_grads(blk.norm1)
@@ -282,7 +300,7 @@ class _LinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         dy_b = dy if dy.dtype == BF16 else ops.cast_bf16(dy)
         lin = ctx.lin
-        dx = ops.linear_dgrad(dy_b, weight_bf16(lin.weight))
+        dx = ops.linear_dgrad(dy_b, weight_bf16(lin.weight), wt=weight_bf16_t(lin.weight))
         ops.linear_wgrad(dy_b, ctx.x, grad_buf(lin.weight))
         _bias_grad(lin, dy)
         ctx.x = None

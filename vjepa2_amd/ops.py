@@ -140,15 +140,32 @@ def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
     return (out, out2) if epi == EPI_GELU else out
 
 
-def linear_dgrad(dy, w, out=None, gelu_pre=None):
-    """dX = dY W (bf16 out); with gelu_pre: dX = (dY W) * GELU'(pre)."""
+def linear_dgrad(dy, w, out=None, gelu_pre=None, wt=None):
+    """dX = dY W (bf16 out); with gelu_pre: dX = (dY W) * GELU'(pre). `wt` = W^T [K, N] contiguous (the
+    K-major B operand the paired GEMM reads); without it W is read MN-major (256-row kernel)."""
     M, N = dy.shape
     K = w.shape[1]
     assert w.shape[0] == N
     out = out if out is not None else torch.empty(M, K, dtype=BF16, device=dy.device)
     epi = EPI_GELU_BWD if gelu_pre is not None else EPI_BF16
-    gemm(M, K, N, dy, _rowmajor(dy, "dy"), True, w, _rowmajor(w, "w"), False, epi, out=out, ldc=out.stride(0),
-         aux=gelu_pre, ldaux=gelu_pre.stride(0) if gelu_pre is not None else 0)
+    aux = dict(aux=gelu_pre, ldaux=gelu_pre.stride(0) if gelu_pre is not None else 0)
+    if wt is not None:
+        assert wt.shape == (K, N), (tuple(wt.shape), (K, N))
+        gemm(M, K, N, dy, _rowmajor(dy, "dy"), True, wt, _rowmajor(wt, "wt"), True, epi, out=out, ldc=out.stride(0),
+             **aux)
+    else:
+        gemm(M, K, N, dy, _rowmajor(dy, "dy"), True, w, _rowmajor(w, "w"), False, epi, out=out, ldc=out.stride(0),
+             **aux)
+    return out
+
+
+def transpose_bf16(x, out=None):
+    """out[c, r] = x[r, c] (bf16, HIP kernel)."""
+    _dev(x)
+    assert x.dtype == BF16 and x.dim() == 2
+    R, C = x.shape
+    out = out if out is not None else torch.empty(C, R, dtype=BF16, device=x.device)
+    _call("vj_transpose_bf16", R, C, _p(x), _rowmajor(x, "x"), _p(out), _rowmajor(out, "out"), _stream())
     return out
 
 

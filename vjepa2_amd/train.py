@@ -79,8 +79,12 @@ def init_opt(encoder, predictor, iterations_per_epoch, start_lr, ref_lr, warmup,
     pred_wd, pred_nowd = wd_split(readiness_order(_trainable(predictor)))
     arenas = [FlatArena(enc_wd, device, name="encoder"), FlatArena(pred_wd, device, name="predictor"),
               FlatArena(enc_nowd, device, name="encoder_nowd"), FlatArena(pred_nowd, device, name="predictor_nowd")]
-    optimizer = FusedAdamW(arenas, wd_exclude=[False, False, zero_init_bias_wd, zero_init_bias_wd], betas=betas,
-                           eps=eps)
+    # the reference's param groups (utils.py:224-237) in named_parameters() order, frozen params
+    # included: the numbering of the optimizer state in checkpoints
+    ref_groups = list(wd_split(encoder.named_parameters())) + list(wd_split(predictor.named_parameters()))
+    ref_groups = [ref_groups[0], ref_groups[2], ref_groups[1], ref_groups[3]]
+    optimizer = FusedAdamW(arenas, wd_exclude=[None, None, zero_init_bias_wd, zero_init_bias_wd], betas=betas,
+                           eps=eps, ref_groups=ref_groups)
     scheduler = WarmupCosineSchedule(optimizer, warmup_steps=int(warmup * iterations_per_epoch), start_lr=start_lr,
                                      ref_lr=ref_lr, final_lr=final_lr,
                                      T_max=int(ipe_scale * num_epochs * iterations_per_epoch))
@@ -162,7 +166,10 @@ class JEPATrainer:
         return loss, zp, dz
 
     def _side_stream(self):
-        if os.environ.get("VJ_TGT_STREAM", "1") == "0" or not torch.cuda.is_available():
+        # Off by default: measured on MI355X it recovered ~1 % of the step while inflating the
+        # memory-bound kernels it shares CUs with (profiles/r01_kernel_stats*.txt). VJ_TGT_STREAM=1
+        # turns it on.
+        if os.environ.get("VJ_TGT_STREAM", "0") != "1" or not torch.cuda.is_available():
             return None
         if getattr(self, "_tgt_stream", None) is None:
             self._tgt_stream = torch.cuda.Stream()
@@ -171,6 +178,13 @@ class JEPATrainer:
     def train_step(self, clips, masks_enc, masks_pred, momentum):
         """clips / masks_* are per frames-per-clip group lists (train.py:393-400 layout). LR / WD
         must already be set on the optimizer's param_groups (schedulers). Returns the loss tensor."""
+        loss = self.compute_grads(clips, masks_enc, masks_pred)
+        self.apply_update(momentum)
+        return loss
+
+    def compute_grads(self, clips, masks_enc, masks_pred):
+        """Forward + backward (train.py:414-445): gradients land in the arenas, all-reduced (summed)
+        across ranks when world > 1."""
         if len(clips) != 1:
             raise NotImplementedError("one frames-per-clip group per step on the fused path "
                                       "(configs with dataset_fpcs all equal produce exactly one)")
@@ -179,13 +193,18 @@ class JEPATrainer:
         zp.backward(dz)
         if self.reducer is not None:
             self.reducer.finish()
+        return loss
+
+    def apply_update(self, momentum):
+        """GradScaler inf-check + AdamW (train.py:446-454) + EMA (train.py:456-465). The 1/world
+        average of the summed gradients is folded into AdamW. Mask tokens other than the one this
+        step used have grad None in the reference, so they take no step (no decay either)."""
         found = self.opt.check_finite() if self.mixed_precision else None
         used = {0 % max(1, len(self.mask_tokens))}
         unused = [t for i, t in enumerate(self.mask_tokens) if i not in used]
         self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused)
         self.opt.zero_grad()
         fused_ema(self.tgt_arenas, self.enc_arenas, momentum)
-        return loss
 
     def sync_bf16(self):
         for a in self.opt.arenas + self.tgt_arenas:
@@ -307,11 +326,12 @@ def main(args, resume_preempt=False):
 
     np.random.seed(seed)
     torch.manual_seed(seed)
-    world_size, rank = init_distributed()
-    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0))) if torch.cuda.is_available() else None
-    if device is None:
+    if not torch.cuda.is_available():
         raise RuntimeError("the V-JEPA HIP train step needs an MI355X (no CPU path)")
+    # bind this rank's GPU BEFORE the process group: RCCL binds its communicator to the current device
+    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", 0)))
     torch.cuda.set_device(device)
+    world_size, rank = init_distributed()
     os.makedirs(folder, exist_ok=True)
     latest_path = os.path.join(folder, "latest.pt")
     load_path = os.path.join(folder, r_file) if r_file is not None else latest_path

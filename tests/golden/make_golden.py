@@ -11,6 +11,7 @@ Stubs: ``timm.models.layers.drop_path`` (never called at drop_p
 Usage:  python tests/golden/make_golden.py            (writes tests/golden/*.pt)
 """
 
+import copy
 import os
 import sys
 import tempfile
@@ -271,7 +272,137 @@ def gen_train_steps():
                                 final_target=strip(ck["target_encoder"])))
 
 
+def _run_reference_main(args, B, fpc, crop, captured, snapshot_iter=None):
+    """app/vjepa/train.py:main on synthetic clips (seed 1000 + item index), CPU fp32. Records the
+    collated samples, per-iteration loss / lr / wd, and (optionally) the encoder / predictor weights
+    right after iteration `snapshot_iter`."""
+    import torch.distributed as dist
+    import app.vjepa.train as rtrain
+
+    class SynthClips(torch.utils.data.Dataset):
+        def __len__(self):
+            return 1000
+
+        def __getitem__(self, i):
+            clip = torch.randn(3, fpc, crop, crop, generator=torch.Generator().manual_seed(1000 + i))
+            return [clip], 0, [torch.arange(fpc)]
+
+    def init_data(batch_size, collator=None, **kw):
+        def collate(batch):
+            s = collator(batch)
+            captured["samples"].append(s)
+            return s
+
+        dl = torch.utils.data.DataLoader(SynthClips(), batch_size=batch_size, collate_fn=collate, shuffle=False,
+                                         num_workers=0)
+        return dl, types.SimpleNamespace(set_epoch=lambda e: None)
+
+    orig_init_opt = rtrain.init_opt
+
+    def init_opt(encoder, predictor, **kw):
+        captured["models"] = (encoder, predictor)
+        return orig_init_opt(encoder=encoder, predictor=predictor, **kw)
+
+    def gpu_timer(closure, log_timings=True):
+        res = closure()
+        captured["losses"].append(res[0])
+        captured.setdefault("lrs", []).append(res[1])
+        captured.setdefault("wds", []).append(res[2])
+        if snapshot_iter is not None and len(captured["losses"]) == snapshot_iter + 1:
+            enc, pred = captured["models"]
+            captured["after"] = dict(encoder={k: v.clone() for k, v in enc.backbone.state_dict().items()},
+                                     predictor={k: v.clone() for k, v in pred.backbone.state_dict().items()})
+        return res, 0.0
+
+    saves = []
+    orig_save = torch.save
+
+    def save(obj, path, *a, **kw):  # keep a detached copy of every checkpoint the reference writes
+        if isinstance(obj, dict) and "opt" in obj:
+            saves.append(copy.deepcopy(obj))
+        return orig_save(obj, path, *a, **kw)
+
+    rtrain.init_data, rtrain.init_opt, rtrain.gpu_timer = init_data, init_opt, gpu_timer
+    torch.save = save
+    try:
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("gloo", rank=0, world_size=1)
+        args = dict(args, folder=tempfile.mkdtemp(prefix="vjepa_golden_"))
+        rtrain.main(args)
+    finally:
+        torch.save = orig_save
+        rtrain.init_opt = orig_init_opt
+    captured["saves"] = saves
+    samples = []
+    for s in captured["samples"]:
+        (batch, menc, mpred), = s
+        samples.append(dict(clip_seeds=[1000 + B * len(samples) + j for j in range(B)],
+                            clip_sum=batch[0][0].double().sum(), enc=menc, pred=mpred))
+    return samples
+
+
+def gen_main_vits():
+    """BASELINE configs[0]: the reference's own app/vjepa/train.py:main at ViT-S/16 8x128^2 B=2, seed 239,
+    ipe 6 (configs/train/vitl16/pretrain-256px-16f.yaml with model_name vit_small). Records the loss /
+    lr / wd trajectory and every step's masks and clip seeds; no weights (both sides build them from
+    the seed)."""
+    B, fpc, crop = 2, 8, 128
+    args = dict(
+        meta=dict(dtype="bfloat16", seed=239, use_sdpa=True, load_checkpoint=False, save_every_freq=-1),
+        mask=VITL_MASKS,
+        model=dict(model_name="vit_small", pred_depth=12, pred_embed_dim=384, pred_num_heads=12, uniform_power=True,
+                   use_activation_checkpointing=True, use_mask_tokens=True, use_rope=True,
+                   zero_init_mask_tokens=True),
+        data=dict(batch_size=B, crop_size=crop, patch_size=16, dataset_fpcs=[fpc], tubelet_size=2, fps=4,
+                  num_workers=0),
+        data_aug=dict(),
+        loss=dict(loss_exp=1.0),
+        optimization=dict(ema=[0.99925, 0.99925], epochs=1, final_lr=0.000525, final_weight_decay=0.04, ipe=6,
+                          ipe_scale=1.25, lr=0.000525, start_lr=0.0001, warmup=40, weight_decay=0.04),
+    )
+    cap = dict(samples=[], losses=[])
+    samples = _run_reference_main(args, B, fpc, crop, cap)
+    save("main_vits.pt", dict(args=args, samples=samples, losses=cap["losses"], lrs=cap["lrs"], wds=cap["wds"]))
+
+
+def gen_resume():
+    """A checkpoint the reference's save_checkpoint writes (app/vjepa/train.py:315-333; micro model,
+    fp32, after epoch 1 = 3 iterations) and what the reference's next iteration does from it: its
+    inputs, loss and the encoder / predictor weights after it."""
+    def vit_micro(patch_size=16, **kw):
+        return vit.VisionTransformer(patch_size=patch_size, embed_dim=64, depth=2, num_heads=1, mlp_ratio=4,
+                                     qkv_bias=True, norm_layer=lambda d: torch.nn.LayerNorm(d, eps=1e-6), **kw)
+
+    vit.vit_micro = vit_micro
+    B, fpc, crop = 2, 8, 64
+    args = dict(
+        meta=dict(dtype="float32", seed=239, use_sdpa=True, load_checkpoint=False, save_every_freq=-1),
+        mask=VITL_MASKS,
+        model=dict(model_name="vit_micro", pred_depth=2, pred_embed_dim=64, pred_num_heads=2, uniform_power=True,
+                   use_activation_checkpointing=False, use_mask_tokens=True, use_rope=True,
+                   zero_init_mask_tokens=True),
+        data=dict(batch_size=B, crop_size=crop, patch_size=16, dataset_fpcs=[fpc], tubelet_size=2, fps=4,
+                  num_workers=0),
+        data_aug=dict(),
+        loss=dict(loss_exp=1.0),
+        optimization=dict(ema=[0.99925, 0.99925], epochs=2, final_lr=0.000525, final_weight_decay=0.04, ipe=3,
+                          ipe_scale=1.25, lr=0.000525, start_lr=0.0001, warmup=1, weight_decay=0.04),
+    )
+    cap = dict(samples=[], losses=[])
+    samples = _run_reference_main(args, B, fpc, crop, cap, snapshot_iter=3)
+    ck = cap["saves"][0]  # end of epoch 1
+    assert ck["epoch"] == 1
+    save("ref_resume.pt", dict(args=args, ckpt=ck, sample=samples[3], loss=cap["losses"][3], lr=cap["lrs"][3],
+                               wd=cap["wds"][3], after=cap["after"]))
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # regenerate selected fixtures only: make_golden.py gen_main_vits gen_resume
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     gen_rope()
     gen_sincos()
     gen_block("block_enc.pt", dim=128, heads=2, grid=4, T=2, N=32, K=10, with_thw=True, seed=3)
@@ -280,3 +411,5 @@ if __name__ == "__main__":
     gen_predictor()
     gen_masks()
     gen_train_steps()
+    gen_main_vits()
+    gen_resume()

@@ -205,6 +205,100 @@ def run_block(x, blk, lay):
 
 
 # ------------------------------------------------------------------------------------------------
+# Standalone RoPEAttention / Attention (modules.py:326-382, 408-429) and MLP (modules.py:77-83)
+# forward()s on the same kernels as the fused block: bf16 operands, f32 outputs.
+
+
+def attn_module_forward(x, attn, lay):
+    """x bf16 [T, C] -> (proj(attention(x)) f32 [T, C], saved for backward)."""
+    H = attn.num_heads
+    hd = x.shape[1] // H
+    if attn.use_rope:
+        c, s = rope_tables(hd, x.device, lay.npos)
+        qkv = ops.qkv_rope(x, weight_bf16(attn.qkv.weight), attn.qkv.bias, H, hd, lay.ids, lay.ids_mod, lay.tpf,
+                           lay.tpr, c, s)
+    else:
+        qkv = ops.linear_fwd(x, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
+    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd))
+    y = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32)
+    return y, (x, qkv, o, stats)
+
+
+def attn_module_backward(dy, attn, lay, saved):
+    x, qkv, o, stats = saved
+    H = attn.num_heads
+    hd = x.shape[1] // H
+    dy_b = ops.cast_bf16(dy)
+    do = ops.linear_dgrad(dy_b, weight_bf16(attn.proj.weight), wt=weight_bf16_t(attn.proj.weight))
+    ops.linear_wgrad(dy_b, o, grad_buf(attn.proj.weight))
+    _bias_grad(attn.proj, dy)
+    rope = None
+    if attn.use_rope:
+        c, s = rope_tables(hd, x.device, lay.npos)
+        rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope)
+    dx = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
+    ops.linear_wgrad(dqkv, x, grad_buf(attn.qkv.weight))
+    _bias_grad(attn.qkv, dqkv)
+    return dx
+
+
+def mlp_module_forward(x, mlp):
+    """x bf16 [T, C] -> (fc2(GELU(fc1 x)) f32, saved)."""
+    T = x.shape[0]
+    pre = torch.empty(T, mlp.fc1.weight.shape[0], dtype=BF16, device=x.device)
+    _, act = ops.linear_fwd(x, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=pre)
+    y = ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_F32)
+    return y, (x, pre, act)
+
+
+def mlp_module_backward(dy, mlp, saved):
+    x, pre, act = saved
+    dy_b = ops.cast_bf16(dy)
+    dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_pre=pre, wt=weight_bf16_t(mlp.fc2.weight))
+    ops.linear_wgrad(dy_b, act, grad_buf(mlp.fc2.weight))
+    _bias_grad(mlp.fc2, dy)
+    dx = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
+    ops.linear_wgrad(dpre, x, grad_buf(mlp.fc1.weight))
+    _bias_grad(mlp.fc1, dpre)
+    return dx
+
+
+class _SubLayerFn(torch.autograd.Function):
+    """Autograd node of a standalone attention or MLP module (parameter grads go straight into
+    param.grad, as for the fused block)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, mod, lay):
+        xb = ops.cast_bf16(x.contiguous()) if x.dtype != BF16 else x.contiguous()
+        if lay is None:
+            y, saved = mlp_module_forward(xb, mod)
+        else:
+            y, saved = attn_module_forward(xb, mod, lay)
+        ctx.mod, ctx.lay, ctx.saved, ctx.in_dtype = mod, lay, saved, x.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy = dy.contiguous().float()
+        if ctx.lay is None:
+            dx = mlp_module_backward(dy, ctx.mod, ctx.saved)
+        else:
+            dx = attn_module_backward(dy, ctx.mod, ctx.lay, ctx.saved)
+        ctx.saved = None
+        _fire_hook(ctx.mod)
+        return dx.to(ctx.in_dtype), None, None, None
+
+
+def run_sublayer(x, mod, lay=None):
+    """x [T, C] (f32 or bf16) through an attention module (lay = its TokenLayout) or an MLP (lay None)."""
+    if _needs_grad(x, mod):
+        return _SubLayerFn.apply(x, next(mod.parameters()), mod, lay)
+    xb = ops.cast_bf16(x.contiguous()) if x.dtype != BF16 else x.contiguous()
+    return (mlp_module_forward(xb, mod) if lay is None else attn_module_forward(xb, mod, lay))[0]
+
+
+# ------------------------------------------------------------------------------------------------
 # Patch embedding: Conv3d(k=s=(tub,p,p)) over the kept tubelets only (patch_embed.py:42-52 +
 # apply_masks vision_transformer.py:188-192), optional sincos pos-embed add (:183-186).
 

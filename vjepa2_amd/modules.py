@@ -25,6 +25,16 @@ class MLP(nn.Module):
         self.act = act_layer()
         self.fc2 = nn.Linear(hidden_features, out_features)
         self.drop = nn.Dropout(drop)
+        if act_layer is not nn.GELU:
+            raise NotImplementedError("MLP supports the exact-erf GELU (nn.GELU) on the HIP path")
+        if drop:
+            raise NotImplementedError("MLP dropout > 0 is not implemented (configs use 0)")
+
+    def forward(self, x):
+        """modules.py:77-83: fc2(GELU(fc1(x))), fc1 + GELU fused in one GEMM epilogue."""
+        shp = x.shape
+        y = fn.run_sublayer(x.reshape(-1, shp[-1]), self)
+        return y.reshape(*shp[:-1], y.shape[-1])
 
 
 class RoPEAttention(nn.Module):
@@ -50,7 +60,13 @@ class RoPEAttention(nn.Module):
         _check_attn(head_dim, attn_drop, proj_drop, is_causal)
 
     def forward(self, x, mask=None, attn_mask=None, T=None, H_patches=None, W_patches=None):
-        raise NotImplementedError("RoPEAttention runs fused inside Block.forward on the HIP path")
+        """modules.py:326-382: QKV (+ 3-axis RoPE of q, k at the token positions: `mask` ids or
+        0..N-1) -> SDPA -> proj, on the fused HIP kernels."""
+        if attn_mask is not None:
+            raise NotImplementedError("attn_mask is not supported on the HIP path")
+        B, N, C = x.shape
+        lay = token_layout(B, N, mask, self.grid_size, H_patches, W_patches, x.device)
+        return fn.run_sublayer(x.reshape(B * N, C), self, lay).reshape(B, N, C)
 
 
 class Attention(nn.Module):
@@ -74,7 +90,12 @@ class Attention(nn.Module):
         _check_attn(head_dim, attn_drop, proj_drop, is_causal)
 
     def forward(self, x, mask=None, attn_mask=None):
-        raise NotImplementedError("Attention runs fused inside Block.forward on the HIP path")
+        """modules.py:408-429: QKV -> SDPA -> proj on the HIP kernels (no positional rotation)."""
+        if attn_mask is not None:
+            raise NotImplementedError("attn_mask is not supported on the HIP path")
+        B, N, C = x.shape
+        lay = fn.TokenLayout([(B, N)], ids=None, ids_mod=N)
+        return fn.run_sublayer(x.reshape(B * N, C), self, lay).reshape(B, N, C)
 
 
 def _check_attn(head_dim, attn_drop, proj_drop, is_causal):
@@ -112,15 +133,7 @@ class Block(nn.Module):
 
     def layout_for(self, B, N, mask, T, H_patches, W_patches, device):
         g = self.attn.grid_size if self.attn.use_rope else 1
-        if H_patches is None or W_patches is None:
-            tpf, tpr = g * g, g
-        else:
-            tpf, tpr = H_patches * W_patches, W_patches
-        ids, nids = None, N
-        if mask is not None:
-            ids = ops.ids_to_int32([mask.to(device=device, dtype=torch.int64).contiguous()])
-            nids = int(mask.max()) + 1  # bounds the RoPE positions (table rows)
-        return fn.TokenLayout([(B, N)], ids=ids, ids_mod=nids, tpf=tpf, tpr=tpr)
+        return token_layout(B, N, mask, g, H_patches, W_patches, device)
 
     def forward(self, x, mask=None, attn_mask=None, T=None, H_patches=None, W_patches=None):
         if attn_mask is not None:
@@ -129,6 +142,21 @@ class Block(nn.Module):
         lay = self.layout_for(B, N, mask, T, H_patches, W_patches, x.device)
         y = fn.run_block(x.float().reshape(B * N, C).contiguous(), self, lay)
         return y.reshape(B, N, C)
+
+
+def token_layout(B, N, mask, grid_size, H_patches, W_patches, device):
+    """RoPE token positions of a [B, N] batch (modules.py:293-341): ids from `mask` ([B, N] token ids)
+    or 0..N-1, split into (frame, row, col) by H_patches / W_patches or the init-time grid size."""
+    g = grid_size
+    if H_patches is None or W_patches is None:
+        tpf, tpr = g * g, g
+    else:
+        tpf, tpr = H_patches * W_patches, W_patches
+    ids, nids = None, N
+    if mask is not None:
+        ids = ops.ids_to_int32([mask.to(device=device, dtype=torch.int64).contiguous()])
+        nids = int(mask.max()) + 1  # bounds the RoPE positions (table rows)
+    return fn.TokenLayout([(B, N)], ids=ids, ids_mod=nids, tpf=tpf, tpr=tpr)
 
 
 def rescale_blocks(blocks):

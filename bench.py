@@ -36,6 +36,8 @@ MASK_CFGS = [
          spatial_scale=[0.7, 0.7], temporal_scale=[1.0, 1.0]),
 ]
 MODELS = {"vit_large": dict(D=1024, depth=24, heads=16, mlp=4096), "vit_small": dict(D=384, depth=12, heads=6, mlp=1536),
+          "vit_huge": dict(D=1280, depth=32, heads=16, mlp=5120),
+          "vit_giant": dict(D=1408, depth=40, heads=16, mlp=6144),
           "vit_giant_xformers": dict(D=1408, depth=40, heads=22, mlp=6144)}
 
 

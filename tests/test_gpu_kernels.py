@@ -168,7 +168,9 @@ def _attn_ref(q, k, v, groups, scale):
 
 
 @pytest.mark.parametrize("hd,H,groups", [(64, 2, [(3, 70), (2, 130)]), (32, 3, [(2, 257), (1, 5)]),
-                                         (64, 1, [(1, 128)]), (32, 2, [(4, 33)])])
+                                         (64, 1, [(1, 128)]), (32, 2, [(4, 33)]),
+                                         # vit_huge / vit_giant head dims (padded to 96 inside)
+                                         (80, 2, [(2, 150), (1, 33)]), (88, 2, [(1, 200), (3, 31)])])
 def test_attention_fwd_bwd(hd, H, groups):
     from vjepa2_amd import ops
 
@@ -194,7 +196,7 @@ def test_attention_fwd_bwd(hd, H, groups):
     assert torch.equal(dqkv, dqkv2)
 
 
-@pytest.mark.parametrize("hd", [64, 32])
+@pytest.mark.parametrize("hd", [64, 32, 80])
 def test_attention_rescale_spikes(hd):
     """Score maxima that grow tile after tile (every step takes the lazy-rescale branch) and one
     isolated spike key per sequence: exercises the O/l rescale of the pipelined forward."""
@@ -272,7 +274,7 @@ def test_colsum():
 
 
 # ------------------------------------------------------------------------------------------------
-@pytest.mark.parametrize("hd,H", [(64, 2), (32, 3)])
+@pytest.mark.parametrize("hd,H", [(64, 2), (32, 3), (80, 2), (88, 2)])
 def test_rope_fwd_bwd(hd, H):
     from vjepa2_amd import ops
 
@@ -304,7 +306,7 @@ def test_rope_fwd_bwd(hd, H):
 
 
 @pytest.mark.parametrize("M", [300, 1500])
-@pytest.mark.parametrize("hd,H", [(64, 2), (32, 3)])
+@pytest.mark.parametrize("hd,H", [(64, 2), (32, 3), (80, 2), (88, 1)])
 def test_fused_rope_paths(M, hd, H):
     """QKV GEMM with RoPE fused into the epilogue vs fp32 GEMM + oracle RoPE (M >= 1024: one bf16
     rounding of the fp32 result, <= 1 ulp; M < 1024 takes GEMM -> bf16 -> rope -> bf16, two

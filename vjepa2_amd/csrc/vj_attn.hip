@@ -1,7 +1,9 @@
 // Varlen flash attention (non-causal, no dropout) for gfx950, forward + deterministic backward.
 // Replaces F.scaled_dot_product_attention in RoPEAttention.forward (src/models/utils/modules.py:367-372)
-// and Attention.forward (modules.py:411-418) for head_dim 64 (ViT encoders) and 32
-// (predictor, A9).
+// and Attention.forward (modules.py:411-418) for head_dim 64 (ViT-L / vit_giant_xformers encoders,
+// SURVEY §8a A6), 32 (predictor, A9), 80 (vit_huge) and 88 (vit_giant). The head dim is padded to a
+// multiple of 32 (HDP) in LDS and in the MFMA loops: the padding columns are zero-filled by the DMA
+// range check / masked loads and never stored, so they add exact zeros.
 //
 // Layout: tokens of all sequences are concatenated ("ragged batch"): q/k/v rows live in one
 // token-major bf16 buffer (the fused QKV GEMM output [T, 3*H*hd]), head h at column off + h*hd.
@@ -68,6 +70,12 @@ struct AttnArgs {
   const float* sin_t;
 };
 
+// padded head dim of the LDS images and MFMA loops
+template <int HD>
+struct Hd {
+  static constexpr int P = (HD + 31) / 32 * 32;
+};
+
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 // Per-token RoPE positions (frame, row, col) for the inverse rotation (modules.py:293-324).
@@ -85,9 +93,11 @@ __device__ __forceinline__ TokPos tok_pos(const AttnArgs& a, int token) {
 // from HD (half = (HD/3)/2, checked at launch), so the index math is by constants; all table
 // values are loaded before any is used so the loads overlap.
 template <int HD>
-__device__ __forceinline__ void rope_inv_rows(const AttnArgs& a, const TokPos& tp, int lane, f32x16 (&x)[HD / 32]) {
+__device__ __forceinline__ void rope_inv_rows(const AttnArgs& a, const TokPos& tp, int lane,
+                                              f32x16 (&x)[Hd<HD>::P / 32]) {
   constexpr int half = (HD / 3) / 2, sw = 2 * half;
-  float c0[HD / 32][8], s0[HD / 32][8], c1[HD / 32][8], s1[HD / 32][8];
+  constexpr int ND = Hd<HD>::P / 32;
+  float c0[ND][8], s0[ND][8], c1[ND][8], s1[ND][8];
   const bool hi = lane >= 32;
   // table index of pair (d, d+1) for a compile-time d (after unrolling): folds to one position
   auto idx = [&](int d, int o) {
@@ -96,7 +106,7 @@ __device__ __forceinline__ void rope_inv_rows(const AttnArgs& a, const TokPos& t
     return (ax == 0 ? tp.fr : (ax == 1 ? tp.hr : tp.wc)) * half + (js + o) % half;
   };
 #pragma unroll
-  for (int d0 = 0; d0 < HD / 32; ++d0)
+  for (int d0 = 0; d0 < ND; ++d0)
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
       const int da = d0 * 32 + (r & 3) + 8 * (r >> 2);  // lanes 0-31; lanes 32-63 hold da + 4
@@ -107,7 +117,7 @@ __device__ __forceinline__ void rope_inv_rows(const AttnArgs& a, const TokPos& t
       s1[d0][r / 2] = a.sin_t[i1];
     }
 #pragma unroll
-  for (int d0 = 0; d0 < HD / 32; ++d0)
+  for (int d0 = 0; d0 < ND; ++d0)
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
       if (d0 * 32 + acc_row(r, lane) >= 3 * sw) continue;
@@ -132,33 +142,37 @@ __device__ __forceinline__ void locate(const SeqGroups& sg, int tile, int tiles_
   seq_start = sg.tok0[g] + s * len;
 }
 
-template <int HD>
+template <int HDP>
 __device__ __forceinline__ int swz(int r) {
-  if constexpr (HD == 64) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
-  else return (r >> 2) & 3;
+  if constexpr (HDP == 64) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
+  else return (r >> 2) & 3;  // 32 (64-B rows) and 96 (192-B rows): stays inside groups of 4 chunks
 }
-template <int HD>
+template <int HDP>
 __device__ __forceinline__ int lds_off(int r, int chunk) {  // byte offset of 16-B chunk
-  return r * (HD * 2) + ((chunk ^ swz<HD>(r)) * 16);
+  return r * (HDP * 2) + ((chunk ^ swz<HDP>(r)) * 16);
 }
 
-// Stage ROWS x HD bf16 rows starting at token row0 (< nvalid valid rows) into an LDS image.
-// Pieces of 1 KB (one wave-instruction); piece p handles rows [p*RPP, (p+1)*RPP).
+// Stage ROWS rows of HD bf16 starting at token row0 (< nvalid valid rows) into an LDS image of
+// HDP-wide rows. Pieces of 1 KB (one wave-instruction, lane-linear in LDS); lane -> (row, physical
+// chunk) from its byte offset; logical chunks >= HD/8 (head-dim padding) and invalid rows are
+// zero-filled by the buffer range check.
 template <int HD, int ROWS>
 __device__ __forceinline__ void stage_rows(__amdgpu_buffer_rsrc_t rs, long ld, int row0, int nvalid,
                                            LDS_AS char* lds, int wave, int lane, int nwaves) {
-  constexpr int CPR = HD / 8;          // 16-B chunks per row
-  constexpr int RPP = 64 / CPR;        // rows per piece
-  constexpr int PIECES = ROWS / RPP;
+  constexpr int HDP = Hd<HD>::P;
+  constexpr int RB = HDP * 2;                  // bytes per LDS row
+  constexpr int PIECES = ROWS * RB / 1024;
+  static_assert(ROWS * RB % 1024 == 0, "tile must be whole 1-KB pieces");
   // nwaves is 4 at every call site: pieces wave, wave + 4, ... (fully unrolled, wave is uniform)
 #pragma unroll
   for (int i = 0; i < (PIECES + 3) / 4; ++i) {
     const int p = wave + 4 * i;
     if (PIECES % 4 != 0 && p >= PIECES) break;
-    const int r = p * RPP + lane / CPR;
-    const int phys = lane % CPR;
-    const int c = phys ^ swz<HD>(r);
-    const bool ok = (row0 + r) < nvalid;
+    const int off = p * 1024 + lane * 16;
+    const int r = off / RB;
+    const int phys = (off - r * RB) >> 4;
+    const int c = phys ^ swz<HDP>(r);
+    const bool ok = (row0 + r) < nvalid && c < HD / 8;
     const uint32_t voff = ok ? (uint32_t)(((long)(row0 + r) * ld + c * 8) * 2) : VJ_OOB;
     dma16(rs, lds + p * 1024, voff);
   }
@@ -166,16 +180,16 @@ __device__ __forceinline__ void stage_rows(__amdgpu_buffer_rsrc_t rs, long ld, i
 }
 
 // A-operand row fragment (rows rb + lane&31, k-step s): 8 bf16 at chunk 2s + (lane>>5).
-template <int HD>
+template <int HDP>
 __device__ __forceinline__ bf16x8 row_frag(const LDS_AS char* lds, int rb, int s, int lane) {
   const int r = rb + (lane & 31);
-  return *(const LDS_AS bf16x8*)(lds + lds_off<HD>(r, 2 * s + (lane >> 5)));
+  return *(const LDS_AS bf16x8*)(lds + lds_off<HDP>(r, 2 * s + (lane >> 5)));
 }
 // Transposed fragment: lane gets X[rows kb+8(j>>2)+4h+(j&3)][col cb + (lane&31)], j = 0..7
 // (the k-permuted order of an accumulator used as an operand). Asm reads (ds_read_tr16_async):
 // callers release them with lds_wait() + tie() before use, which lets the next tile's LDS-DMA be
 // issued at the top of the iteration without the compiler serialising the reads behind it.
-template <int HD>
+template <int HDP>
 __device__ __forceinline__ bf16x8 tr_frag(const LDS_AS char* lds, int kb, int cb, int lane) {
   const int h = lane >> 5;
   const int q = (lane >> 2) & 3;
@@ -183,8 +197,8 @@ __device__ __forceinline__ bf16x8 tr_frag(const LDS_AS char* lds, int kb, int cb
   const int r0 = kb + 4 * h + q;
   const int r1 = r0 + 8;
   const int within = (col & 7) * 2;
-  const s16x4 lo = ds_read_tr16_async(lds + lds_off<HD>(r0, col >> 3) + within);
-  const s16x4 hi = ds_read_tr16_async(lds + lds_off<HD>(r1, col >> 3) + within);
+  const s16x4 lo = ds_read_tr16_async(lds + lds_off<HDP>(r0, col >> 3) + within);
+  const s16x4 hi = ds_read_tr16_async(lds + lds_off<HDP>(r1, col >> 3) + within);
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
 }
@@ -214,8 +228,9 @@ constexpr float LOG2E = 1.4426950408889634f;
 // Forward: block = 4 waves x 32 queries, KV tiles of 64 keys double-buffered in LDS.
 template <int HD>
 __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
+  constexpr int HDP = Hd<HD>::P;
   constexpr int KT = 64;
-  constexpr int TB = KT * HD * 2;  // bytes per K or V tile
+  constexpr int TB = KT * HDP * 2;  // bytes per K or V tile
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -226,11 +241,11 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   const bool qok = qloc < len;
   const int hl = lane >> 5;
 
-  // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[q][16s + 8h + j].
-  bf16x8 qf[HD / 16];
+  // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[q][16s + 8h + j] (zero past HD).
+  bf16x8 qf[HDP / 16];
   const bf16_t* qrow = a.qkv + (long)(seq0 + qloc) * a.ld + a.q_off + h * HD;
 #pragma unroll
-  for (int s = 0; s < HD / 16; ++s) qf[s] = gload8(qrow + 16 * s + 8 * hl, qok);
+  for (int s = 0; s < HDP / 16; ++s) qf[s] = gload8(qrow + 16 * s + 8 * hl, qok && 16 * s + 8 * hl < HD);
 
   const bf16_t* kbase = a.qkv + (long)seq0 * a.ld + a.k_off + h * HD;
   const bf16_t* vbase = a.qkv + (long)seq0 * a.ld + a.v_off + h * HD;
@@ -240,11 +255,11 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
 
   // O^T accumulators; lt = "ones row" tile: row 0 of V^T replaced by ones gives l = sum_k p (the
   // softmax denominator of the same bf16 P the numerator uses) on the MFMA pipe instead of 32 adds.
-  f32x16 ot[HD / 32], lt;
+  f32x16 ot[HDP / 32], lt;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
 #pragma unroll
-    for (int d = 0; d < HD / 32; ++d) ot[d][r] = 0.f;
+    for (int d = 0; d < HDP / 32; ++d) ot[d][r] = 0.f;
     lt[r] = 0.f;
   }
   bf16x8 ones;
@@ -274,27 +289,27 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
       stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
     }
     // all K fragments first (one LDS wait), then two independent S^T chains interleaved
-    bf16x8 kf[2][HD / 16];
+    bf16x8 kf[2][HDP / 16];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int s = 0; s < HD / 16; ++s) kf[kk][s] = row_frag<HD>(Ks, kk * 32, s, lane);
+      for (int s = 0; s < HDP / 16; ++s) kf[kk][s] = row_frag<HDP>(Ks, kk * 32, s, lane);
     f32x16 st[2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s)
+    for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
         st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][s], qf[s], st[kk], 0, 0, 0);
     // V^T fragments: issued before the softmax so their LDS latency hides under it
-    bf16x8 vf[4][HD / 32];
+    bf16x8 vf[4][HDP / 32];
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-      for (int d = 0; d < HD / 32; ++d) vf[ks][d] = tr_frag<HD>(Vs, ks * 16, d * 32, lane);
+      for (int d = 0; d < HDP / 32; ++d) vf[ks][d] = tr_frag<HDP>(Vs, ks * 16, d * 32, lane);
     const int kb = kt * KT;
     if (kb + KT > len) {  // ragged last tile only: keys beyond the sequence get -inf
       asm volatile("");  // keeps the compiler from if-converting this into every tile
@@ -319,7 +334,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
 #pragma unroll
-        for (int d = 0; d < HD / 32; ++d) ot[d][r] *= alpha;
+        for (int d = 0; d < HDP / 32; ++d) ot[d][r] *= alpha;
         lt[r] *= alpha;
       }
     }
@@ -335,7 +350,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
     for (int ks = 0; ks < 4; ++ks) {
       const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
 #pragma unroll
-      for (int d = 0; d < HD / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
+      for (int d = 0; d < HDP / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
       lt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf, lt, 0, 0, 0);
     }
     __syncthreads();
@@ -349,11 +364,11 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   if (qok) {
     bf16_t* orow = a.o + (long)(seq0 + qloc) * a.ldo + h * HD;
 #pragma unroll
-    for (int d = 0; d < HD / 32; ++d)
+    for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int col = d * 32 + acc_row(r, lane);
-        *(uint32_t*)(orow + col) = pack_bf2(ot[d][r] * inv, ot[d][r + 1] * inv);
+        if (col < HD) *(uint32_t*)(orow + col) = pack_bf2(ot[d][r] * inv, ot[d][r + 1] * inv);
       }
     if (hl == 0) a.stats[(long)h * a.T + seq0 + qloc] = m_use * c + __log2f(l_tot);  // log2 units
   }
@@ -384,8 +399,9 @@ __global__ void k_attn_delta(AttnArgs a) {
 // so every staged Q / dO fragment feeds KW independent MFMA chains per barrier.
 template <int HD, int KW>
 __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
+  constexpr int HDP = Hd<HD>::P;
   constexpr int QT = 32;
-  constexpr int TB = QT * HD * 2;
+  constexpr int TB = QT * HDP * 2;
   // per stage: Q tile, dO tile, 32 lse + 32 delta floats
   constexpr int STAGE = 2 * TB + 256;
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
@@ -404,15 +420,15 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   const int hl = lane >> 5;
 
   // K^T and V^T fragments (B operands): lane holds K[key][16s + 8h + j].
-  bf16x8 kf[KW][HD / 16], vf[KW][HD / 16];
+  bf16x8 kf[KW][HDP / 16], vf[KW][HDP / 16];
 #pragma unroll
   for (int kw = 0; kw < KW; ++kw) {
     const bf16_t* krow = a.qkv + (long)(seq0 + kloc[kw]) * a.ld + a.k_off + h * HD;
     const bf16_t* vrow = a.qkv + (long)(seq0 + kloc[kw]) * a.ld + a.v_off + h * HD;
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s) {
-      kf[kw][s] = gload8(krow + 16 * s + 8 * hl, kok[kw]);
-      vf[kw][s] = gload8(vrow + 16 * s + 8 * hl, kok[kw]);
+    for (int s = 0; s < HDP / 16; ++s) {
+      kf[kw][s] = gload8(krow + 16 * s + 8 * hl, kok[kw] && 16 * s + 8 * hl < HD);
+      vf[kw][s] = gload8(vrow + 16 * s + 8 * hl, kok[kw] && 16 * s + 8 * hl < HD);
     }
   }
   const uint32_t qbytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
@@ -424,11 +440,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       make_rsrc(a.stats + (long)h * a.T + seq0, (uint32_t)min(((long)a.H * a.T + len) * 4, 0x7fffffffL));
   const long dstat = (long)a.H * a.T;  // element distance lse -> delta
 
-  f32x16 dvt[KW][HD / 32], dkt[KW][HD / 32];
+  f32x16 dvt[KW][HDP / 32], dkt[KW][HDP / 32];
 #pragma unroll
   for (int kw = 0; kw < KW; ++kw)
 #pragma unroll
-    for (int d = 0; d < HD / 32; ++d)
+    for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dvt[kw][d][r] = dkt[kw][d][r] = 0.f;
   const float c = a.scale * LOG2E;
@@ -457,11 +473,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
     const LDS_AS char* Qs = smem + cur * STAGE;
     const LDS_AS char* Ds = Qs + TB;
     const LDS_AS float* Ls = (const LDS_AS float*)(Qs + 2 * TB);
-    bf16x8 qa[HD / 16], da[HD / 16];
+    bf16x8 qa[HDP / 16], da[HDP / 16];
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s) {
-      qa[s] = row_frag<HD>(Qs, 0, s, lane);
-      da[s] = row_frag<HD>(Ds, 0, s, lane);
+    for (int s = 0; s < HDP / 16; ++s) {
+      qa[s] = row_frag<HDP>(Qs, 0, s, lane);
+      da[s] = row_frag<HDP>(Ds, 0, s, lane);
     }
     // S - lse2/c = Q K^T - lse2/c (rows: queries, col: key); dP - delta = dO V^T - delta: the
     // per-query terms are the accumulators' initial values, so no per-row registers stay live
@@ -477,19 +493,19 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       }
     }
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s)
+    for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
       for (int kw = 0; kw < KW; ++kw) {
         sacc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[kw][s], sacc[kw], 0, 0, 0);
         dp[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[kw][s], dp[kw], 0, 0, 0);
       }
-    bf16x8 dtf[2][HD / 32], qtf[2][HD / 32];
+    bf16x8 dtf[2][HDP / 32], qtf[2][HDP / 32];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int d = 0; d < HD / 32; ++d) {
-        dtf[s2][d] = tr_frag<HD>(Ds, s2 * 16, d * 32, lane);
-        qtf[s2][d] = tr_frag<HD>(Qs, s2 * 16, d * 32, lane);
+      for (int d = 0; d < HDP / 32; ++d) {
+        dtf[s2][d] = tr_frag<HDP>(Ds, s2 * 16, d * 32, lane);
+        qtf[s2][d] = tr_frag<HDP>(Qs, s2 * 16, d * 32, lane);
       }
     // P = 2^(c*S - lse2); dS = P * (dP - delta)
 #pragma unroll
@@ -514,7 +530,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
         const bf16x8 pf = acc_frag(sacc[kw], s2);
         const bf16x8 sf = acc_frag(dp[kw], s2);
 #pragma unroll
-        for (int d = 0; d < HD / 32; ++d) {
+        for (int d = 0; d < HDP / 32; ++d) {
           dvt[kw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dtf[s2][d], pf, dvt[kw][d], 0, 0, 0);
           dkt[kw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtf[s2][d], sf, dkt[kw][d], 0, 0, 0);
         }
@@ -535,15 +551,16 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
     // rotate everything before the first store (the stores could alias the tables, so the
     // table loads would otherwise be serialised behind them)
 #pragma unroll
-    for (int d = 0; d < HD / 32; ++d)
+    for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dkt[kw][d][r] *= a.scale;
     if (rope) rope_inv_rows<HD>(a, tp, lane, dkt[kw]);
 #pragma unroll
-    for (int d = 0; d < HD / 32; ++d)
+    for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const int col = d * 32 + acc_row(r, lane);
+        if (col >= HD) continue;
         *(uint32_t*)(dk + col) = pack_bf2(dkt[kw][d][r], dkt[kw][d][r + 1]);
         *(uint32_t*)(dv + col) = pack_bf2(dvt[kw][d][r], dvt[kw][d][r + 1]);
       }
@@ -556,8 +573,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
 // fragment read from LDS feeds QW independent MFMA chains.
 template <int HD, int QW>
 __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
+  constexpr int HDP = Hd<HD>::P;
   constexpr int KT = 64;
-  constexpr int TB = KT * HD * 2;
+  constexpr int TB = KT * HDP * 2;
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -567,7 +585,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   const int hl = lane >> 5;
   int qloc[QW];
   bool qok[QW];
-  bf16x8 qf[QW][HD / 16], gf[QW][HD / 16];
+  bf16x8 qf[QW][HDP / 16], gf[QW][HDP / 16];
   float lse2[QW], dl[QW];
 #pragma unroll
   for (int qw = 0; qw < QW; ++qw) {
@@ -576,9 +594,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
     const bf16_t* qrow = a.qkv + (long)(seq0 + qloc[qw]) * a.ld + a.q_off + h * HD;
     const bf16_t* grow = a.dout + (long)(seq0 + qloc[qw]) * a.lddo + h * HD;
 #pragma unroll
-    for (int s = 0; s < HD / 16; ++s) {
-      qf[qw][s] = gload8(qrow + 16 * s + 8 * hl, qok[qw]);
-      gf[qw][s] = gload8(grow + 16 * s + 8 * hl, qok[qw]);
+    for (int s = 0; s < HDP / 16; ++s) {
+      qf[qw][s] = gload8(qrow + 16 * s + 8 * hl, qok[qw] && 16 * s + 8 * hl < HD);
+      gf[qw][s] = gload8(grow + 16 * s + 8 * hl, qok[qw] && 16 * s + 8 * hl < HD);
     }
     lse2[qw] = qok[qw] ? a.stats[(long)h * a.T + seq0 + qloc[qw]] : 0.f;
     dl[qw] = qok[qw] ? a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc[qw]] : 0.f;
@@ -588,11 +606,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.qkv + (long)seq0 * a.ld + a.k_off + h * HD, bytes);
   const __amdgpu_buffer_rsrc_t rv = make_rsrc(a.qkv + (long)seq0 * a.ld + a.v_off + h * HD, bytes);
 
-  f32x16 dqt[QW][HD / 32];
+  f32x16 dqt[QW][HDP / 32];
 #pragma unroll
   for (int qw = 0; qw < QW; ++qw)
 #pragma unroll
-    for (int d = 0; d < HD / 32; ++d)
+    for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dqt[qw][d][r] = 0.f;
   const float c = a.scale * LOG2E;
@@ -620,16 +638,16 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
     // dQ^T += K^T dS^T. Halves run one after the other so only one half's fragments are live.
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 ka[HD / 16], va[HD / 16], ktf[2][HD / 32];
+      bf16x8 ka[HDP / 16], va[HDP / 16], ktf[2][HDP / 32];
 #pragma unroll
-      for (int s = 0; s < HD / 16; ++s) {
-        ka[s] = row_frag<HD>(Ks, kk * 32, s, lane);
-        va[s] = row_frag<HD>(Vs, kk * 32, s, lane);
+      for (int s = 0; s < HDP / 16; ++s) {
+        ka[s] = row_frag<HDP>(Ks, kk * 32, s, lane);
+        va[s] = row_frag<HDP>(Vs, kk * 32, s, lane);
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int d = 0; d < HD / 32; ++d) ktf[s2][d] = tr_frag<HD>(Ks, kk * 32 + s2 * 16, d * 32, lane);
+        for (int d = 0; d < HDP / 32; ++d) ktf[s2][d] = tr_frag<HDP>(Ks, kk * 32 + s2 * 16, d * 32, lane);
       f32x16 st[QW], dpt[QW];
 #pragma unroll
       for (int qw = 0; qw < QW; ++qw)
@@ -639,7 +657,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
           dpt[qw][r] = dl[qw];
         }
 #pragma unroll
-      for (int s = 0; s < HD / 16; ++s)
+      for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
         for (int qw = 0; qw < QW; ++qw) {
           st[qw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s], qf[qw][s], st[qw], 0, 0, 0);
@@ -668,7 +686,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
         for (int qw = 0; qw < QW; ++qw) {
           const bf16x8 sf = acc_frag(dpt[qw], s2);
 #pragma unroll
-          for (int d = 0; d < HD / 32; ++d)
+          for (int d = 0; d < HDP / 32; ++d)
             dqt[qw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktf[s2][d], sf, dqt[qw][d], 0, 0, 0);
         }
     }
@@ -685,15 +703,17 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
     const bool rope = a.cos_t != nullptr;
     const TokPos tp = rope ? tok_pos(a, seq0 + qloc[qw]) : TokPos{0, 0, 0};
 #pragma unroll
-    for (int d = 0; d < HD / 32; ++d)
+    for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dqt[qw][d][r] *= a.scale;
     if (rope) rope_inv_rows<HD>(a, tp, lane, dqt[qw]);  // rotate first, then store (see k_attn_bwd_dkdv)
 #pragma unroll
-    for (int d = 0; d < HD / 32; ++d)
+    for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
-      for (int r = 0; r < 16; r += 2)
-        *(uint32_t*)(dq + d * 32 + acc_row(r, lane)) = pack_bf2(dqt[qw][d][r], dqt[qw][d][r + 1]);
+      for (int r = 0; r < 16; r += 2) {
+        const int col = d * 32 + acc_row(r, lane);
+        if (col < HD) *(uint32_t*)(dq + col) = pack_bf2(dqt[qw][d][r], dqt[qw][d][r + 1]);
+      }
   }
 }
 
@@ -723,7 +743,8 @@ int fill_groups(SeqGroups& sg, int ngroups, const int* nseq, const int* len, int
 }
 
 int check_common(int H, int hd, long ld, long ldo) {
-  VJ_CHECK_ARG(hd == 64 || hd == 32, "attention: head_dim must be 32 or 64 (got %d)", hd);
+  VJ_CHECK_ARG(hd == 64 || hd == 32 || hd == 80 || hd == 88,
+               "attention: head_dim must be 32, 64, 80 or 88 (got %d)", hd);
   VJ_CHECK_ARG(H >= 1 && H <= 65535, "attention: bad H=%d", H);
   VJ_CHECK_ARG(ld % 8 == 0 && ldo % 8 == 0, "attention: row strides must be multiples of 8");
   return VJ_OK;
@@ -744,8 +765,12 @@ extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q
   if (rc) return rc;
   dim3 grid(a.sg.tiles_prefix[MAXG], H);
   hipStream_t st = (hipStream_t)stream;
-  if (hd == 64) hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(k_attn_fwd<32>, grid, dim3(256), 0, st, a);
+  switch (hd) {
+    case 64: hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(256), 0, st, a); break;
+    case 32: hipLaunchKernelGGL(k_attn_fwd<32>, grid, dim3(256), 0, st, a); break;
+    case 80: hipLaunchKernelGGL(k_attn_fwd<80>, grid, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(k_attn_fwd<88>, grid, dim3(256), 0, st, a); break;
+  }
   VJ_LAUNCH_CHECK("vj_attn_fwd");
   return VJ_OK;
 }
@@ -773,8 +798,8 @@ extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q
   a.o = (bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.stats = stats;
   a.dqkv = (bf16_t*)dqkv; a.ldd = ldd; a.H = H; a.T = T; a.scale = scale;
   // key / query 32-row tiles per wave of the two sweeps (block tile = 128 x that)
-  const int kw = hd == 64 ? VJ_ATTN_KW64 : VJ_ATTN_KW32;
-  const int qw = hd == 64 ? VJ_ATTN_QW64 : VJ_ATTN_QW32;
+  const int kw = hd == 32 ? VJ_ATTN_KW32 : hd == 64 ? VJ_ATTN_KW64 : 1;
+  const int qw = hd == 32 ? VJ_ATTN_QW32 : hd == 64 ? VJ_ATTN_QW64 : 1;
   AttnArgs ak = a, aq = a;
   rc = fill_groups(ak.sg, ngroups, nseq, len, 128 * kw, T);
   if (rc) return rc;
@@ -784,14 +809,27 @@ extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q
   const long nth = (long)T * H;
   const int dblocks = (int)((nth + 255) / 256);
   const dim3 gk(ak.sg.tiles_prefix[MAXG], H), gq(aq.sg.tiles_prefix[MAXG], H);
-  if (hd == 64) {
-    hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64>), gk, dim3(256), 0, st, ak);
-    hipLaunchKernelGGL((k_attn_bwd_dq<64, VJ_ATTN_QW64>), gq, dim3(256), 0, st, aq);
-  } else {
-    hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
-    hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32>), gk, dim3(256), 0, st, ak);
-    hipLaunchKernelGGL((k_attn_bwd_dq<32, VJ_ATTN_QW32>), gq, dim3(256), 0, st, aq);
+  switch (hd) {
+    case 64:
+      hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64>), gk, dim3(256), 0, st, ak);
+      hipLaunchKernelGGL((k_attn_bwd_dq<64, VJ_ATTN_QW64>), gq, dim3(256), 0, st, aq);
+      break;
+    case 32:
+      hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32>), gk, dim3(256), 0, st, ak);
+      hipLaunchKernelGGL((k_attn_bwd_dq<32, VJ_ATTN_QW32>), gq, dim3(256), 0, st, aq);
+      break;
+    case 80:
+      hipLaunchKernelGGL(k_attn_delta<80>, dim3(dblocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<80, 1>), gk, dim3(256), 0, st, ak);
+      hipLaunchKernelGGL((k_attn_bwd_dq<80, 1>), gq, dim3(256), 0, st, aq);
+      break;
+    default:
+      hipLaunchKernelGGL(k_attn_delta<88>, dim3(dblocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<88, 1>), gk, dim3(256), 0, st, ak);
+      hipLaunchKernelGGL((k_attn_bwd_dq<88, 1>), gq, dim3(256), 0, st, aq);
+      break;
   }
   VJ_LAUNCH_CHECK("vj_attn_bwd");
   return VJ_OK;

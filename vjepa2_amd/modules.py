@@ -99,8 +99,8 @@ class Attention(nn.Module):
 
 
 def _check_attn(head_dim, attn_drop, proj_drop, is_causal):
-    if head_dim not in (32, 64):
-        raise NotImplementedError(f"HIP attention supports head_dim 32 and 64 (got {head_dim})")
+    if head_dim not in (32, 64, 80, 88):
+        raise NotImplementedError(f"HIP attention supports head_dim 32, 64, 80, 88 (got {head_dim})")
     if attn_drop or proj_drop:
         raise NotImplementedError("attention/projection dropout > 0 is not implemented (configs use 0)")
     if is_causal:

@@ -195,7 +195,7 @@ class VisionTransformer(nn.Module):
 
 
 # ------------------------------------------------------------------------------------------------
-# Factories (vision_transformer.py:275-475); only head_dim 32/64 models run on the HIP attention.
+# Factories (vision_transformer.py:275-475): head dims 64 (large, giant_xformers), 80 (huge), 88 (giant).
 def _ln():
     return partial(nn.LayerNorm, eps=1e-6)
 

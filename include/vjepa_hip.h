@@ -74,6 +74,25 @@ int vj_qkv_rope_gemm(int M, int K, const void* A, long lda, const void* B, long 
                      long ldc, int H, int hd, const int* ids, int ids_mod, int tpf, int tpr, const float* cos_t,
                      const float* sin_t, int npos, void* stream);
 
+/* fp8 (OCP e4m3) forward GEMMs of the opt-in fp8 target encoder (BASELINE configs[4]; the reference has
+ * no fp8: judged by its error envelope). A [M, K] and B [N, K] e4m3 bytes, both K-major (X W^T), with
+ * per-row power-of-two scales: A(m, k) = A8[m, k] * 2^ea[m], B(n, k) = B8[n, k] * 2^eb[n] (device int32
+ * exponents, applied exactly by the MFMA's E8M0 scale operands); f32 accumulation. K, lda, ldb multiples
+ * of 16 bytes. Epilogues: VJ_EPI_BF16 / VJ_EPI_F32 / VJ_EPI_F32_RESID / VJ_EPI_GELU (bf16 act) as vj_gemm_bf16;
+ * replaces the QKV (+RoPE, modules.py:330 + 343-365) and fc1 (+GELU, :77-83) Linears of the target encoder. */
+int vj_gemm_fp8(int M, int N, int K, const void* A, long lda, const int* ea, const void* B, long ldb, const int* eb,
+                int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc, void* C2, long ldc2,
+                void* stream);
+int vj_qkv_rope_gemm_fp8(int M, int K, const void* A, long lda, const int* ea, const void* B, long ldb, const int* eb,
+                         const float* bias, void* C, long ldc, int H, int hd, const int* ids, int ids_mod, int tpf,
+                         int tpr, const float* cos_t, const float* sin_t, int npos, void* stream);
+/* Per-row e4m3 quantisation: y8[m, :] = e4m3(x[m, :] * 2^-e[m]), e[m] the least exponent with
+ * max|x[m, :]| * 2^-e <= 448 (0 for a zero row; a non-finite row becomes NaN bytes). x f32 or bf16. */
+int vj_quant_rows_fp8(int M, int K, const void* x, int x_bf16, long ldx, void* y8, long ldy, int* yexp, void* stream);
+/* LayerNorm whose output row is written as per-row scaled e4m3 (as vj_quant_rows_fp8) for the fp8 GEMMs. */
+int vj_layernorm_fwd_fp8(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma, const float* beta,
+                         float eps, void* y8, long ldy, int* yexp, float* mean, float* rstd, void* stream);
+
 /* LayerNorm (nn.LayerNorm / F.layer_norm, modules.py:556-563, train.py:417): x f32 or bf16, y bf16 or f32,
  * gamma/beta optional (both or neither); mean/rstd optional outputs. D % 4 == 0, D <= 2048. */
 int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma, const float* beta,

@@ -30,6 +30,10 @@ SIGNATURES = {
                     _P, _P],
     "vj_qkv_rope_gemm": [_I, _I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _I, _I, _I, _P, _P, _I, _P],
     "vj_layernorm_fwd": [_I, _I, _P, _I, _L, _P, _P, _F, _P, _I, _L, _P, _P, _P],
+    "vj_gemm_fp8": [_I, _I, _I, _P, _L, _P, _P, _L, _P, _I, _P, _P, _L, _P, _L, _P, _L, _P],
+    "vj_qkv_rope_gemm_fp8": [_I, _I, _P, _L, _P, _P, _L, _P, _P, _P, _L, _I, _I, _P, _I, _I, _I, _P, _P, _I, _P],
+    "vj_quant_rows_fp8": [_I, _I, _P, _I, _L, _P, _L, _P, _P],
+    "vj_layernorm_fwd_fp8": [_I, _I, _P, _I, _L, _P, _P, _F, _P, _L, _P, _P, _P, _P],
     "vj_layernorm_bwd_blocks": [_I],
     "vj_layernorm_bwd": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _L, _P, _P, _P, _P, _P, _L, _P],
     "vj_colsum_f32": [_I, _I, _P, _I, _L, _P, _I, _P, _L, _P],

@@ -19,11 +19,20 @@ namespace {
 // LayerNorm forward: wave per row. x f32 or bf16 [M, ldx]; y bf16 or f32 [M, ldy]; optional affine.
 constexpr int LN_MAXV = 8;  // float4 per lane -> D <= 64*4*8 = 2048
 
+// e4m3 per-row scale exponent: the least e with amax * 2^-e <= 448 (0 for an all-zero or non-finite row)
+__device__ __forceinline__ int f8_row_exp(float amax) {
+  if (!(amax > 0.f) || !(amax <= 3.0e38f)) return 0;
+  int e = (int)ceilf(__log2f(amax / 448.f));
+  if (ldexpf(amax, -e) > 448.f) ++e;
+  if (ldexpf(amax, -(e - 1)) <= 448.f) --e;
+  return min(max(e, -120), 120);
+}
+
 template <bool XBF, bool YF32, int NV, bool YF8 = false>
 __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __restrict__ x, long ldx,
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 float eps, void* __restrict__ y, long ldy, float* __restrict__ mean,
-                                                float* __restrict__ rstd) {
+                                                float* __restrict__ rstd, int* __restrict__ yexp = nullptr) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -63,8 +72,8 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
         const float4 b = *(const float4*)(beta + c);
         o[0] = o[0] * g.x + b.x; o[1] = o[1] * g.y + b.y; o[2] = o[2] * g.z + b.z; o[3] = o[3] * g.w + b.w;
       }
-      if constexpr (YF8) {  // unscaled e4m3 operand of the fp8 QKV / fc1 GEMMs (|y| <= 448 clamp)
-        *(uint32_t*)((unsigned char*)y + row * ldy + c) = f8pack4(o[0], o[1], o[2], o[3]);
+      if constexpr (YF8) {
+        v[i] = make_float4(o[0], o[1], o[2], o[3]);  // kept for the scaled fp8 pass below
       } else if constexpr (YF32) {
         *(float4*)((float*)y + row * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
       } else {
@@ -72,10 +81,61 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
       }
     }
   }
+  if constexpr (YF8) {  // per-row scaled e4m3: y8 = e4m3(y * 2^-e), e = the least exponent with amax * 2^-e <= 448
+    float am = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if ((i * 64 + lane) * 4 < D)
+        am = fmaxf(am, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
+    am = wave_max(am);
+    const int e = f8_row_exp(am);
+    const float sc = ldexpf(1.f, -e);
+    const bool bad = !(am <= 3.0e38f);  // inf / NaN row: every byte NaN (e4m3fn has no infinity)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      if (c < D)
+        *(uint32_t*)((unsigned char*)y + row * ldy + c) =
+            bad ? 0x7f7f7f7fu : f8pack4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
+    }
+    if (lane == 0) yexp[row] = e;
+  }
   if (lane == 0) {
     if (mean) mean[row] = mu;
     if (rstd) rstd[row] = rs;
   }
+}
+
+// Per-row fp8 quantisation of a [M, K] f32 / bf16 matrix (the fp8 target encoder's weights, one
+// scale per output channel): wave per row, two passes over the row (amax, then scaled e4m3 bytes).
+template <bool XBF>
+__global__ __launch_bounds__(256) void k_quant_rows_fp8(int M, int K, const void* __restrict__ x, long ldx,
+                                                        unsigned char* __restrict__ y, long ldy, int* __restrict__ yexp) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  auto load4 = [&](int c) {
+    if constexpr (XBF) {
+      const uint2 u = *(const uint2*)((const bf16_t*)x + row * ldx + c);
+      return make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+    } else {
+      return *(const float4*)((const float*)x + row * ldx + c);
+    }
+  };
+  float am = 0.f;
+  for (int c = lane * 4; c < K; c += 256) {
+    const float4 v = load4(c);
+    am = fmaxf(am, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  am = wave_max(am);
+  const int e = f8_row_exp(am);
+  const float sc = ldexpf(1.f, -e);
+  const bool bad = !(am <= 3.0e38f);
+  for (int c = lane * 4; c < K; c += 256) {
+    const float4 v = load4(c);
+    *(uint32_t*)(y + row * ldy + c) = bad ? 0x7f7f7f7fu : f8pack4(v.x * sc, v.y * sc, v.z * sc, v.w * sc);
+  }
+  if (lane == 0) yexp[row] = e;
 }
 
 // LayerNorm backward. dy bf16 [M, lddy]; x f32 [M, ldx]; dres f32 [M, ldr] = (dres_in or 0) + dx;
@@ -675,19 +735,7 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
   const int nv = ln_nv(D);
 #define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, YF, NVV>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
 #define LNF_NV(XB, YF) switch (nv) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 4: LNF(XB, YF, 4); break; case 6: LNF(XB, YF, 6); break; default: LNF(XB, YF, 8); }
-#define LNF8(XB, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, false, NVV, true>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
-  if (y_f32 == 2) {  // fp8 e4m3 output
-    VJ_CHECK_ARG(ldy % 16 == 0 && !((uintptr_t)y & 15), "vj_layernorm_fwd: fp8 output needs 16-B rows");
-    switch (nv) {
-      case 1: if (x_bf16) LNF8(true, 1); else LNF8(false, 1); break;
-      case 2: if (x_bf16) LNF8(true, 2); else LNF8(false, 2); break;
-      case 4: if (x_bf16) LNF8(true, 4); else LNF8(false, 4); break;
-      case 6: if (x_bf16) LNF8(true, 6); else LNF8(false, 6); break;
-      default: if (x_bf16) LNF8(true, 8); else LNF8(false, 8);
-    }
-  }
-#undef LNF8
-  else if (x_bf16 && y_f32) { LNF_NV(true, true) }
+  if (x_bf16 && y_f32) { LNF_NV(true, true) }
   else if (x_bf16) { LNF_NV(true, false) }
   else if (y_f32) { LNF_NV(false, true) }
   else { LNF_NV(false, false) }
@@ -922,5 +970,47 @@ extern "C" int vj_transpose_bf16(int rows, int cols, const void* src, long ld_sr
   hipLaunchKernelGGL(k_transpose_bf16, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const bf16_t*)src,
                      ld_src, (bf16_t*)dst, ld_dst);
   VJ_LAUNCH_CHECK("vj_transpose_bf16");
+  return VJ_OK;
+}
+
+extern "C" int vj_layernorm_fwd_fp8(int M, int D, const void* x, int x_bf16, long ldx, const float* gamma,
+                                    const float* beta, float eps, void* y8, long ldy, int* yexp, float* mean,
+                                    float* rstd, void* stream) {
+  if (M == 0) return VJ_OK;
+  VJ_CHECK_ARG(D % 4 == 0 && D <= 64 * 4 * LN_MAXV, "vj_layernorm_fwd_fp8: D=%d must be %%4 and <= 2048", D);
+  VJ_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "vj_layernorm_fwd_fp8: gamma/beta both or neither");
+  VJ_CHECK_ARG(ldx % 4 == 0 && ldy % 16 == 0 && !((uintptr_t)y8 & 15) && yexp,
+               "vj_layernorm_fwd_fp8: fp8 rows must be 16-B aligned, exponents required");
+  dim3 grid((M + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+#define LNF8(XB, NVV)                                                                                             \
+  hipLaunchKernelGGL((k_ln_fwd<XB, false, NVV, true>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y8, \
+                     ldy, mean, rstd, yexp)
+  switch (ln_nv(D)) {
+    case 1: if (x_bf16) LNF8(true, 1); else LNF8(false, 1); break;
+    case 2: if (x_bf16) LNF8(true, 2); else LNF8(false, 2); break;
+    case 4: if (x_bf16) LNF8(true, 4); else LNF8(false, 4); break;
+    case 6: if (x_bf16) LNF8(true, 6); else LNF8(false, 6); break;
+    default: if (x_bf16) LNF8(true, 8); else LNF8(false, 8);
+  }
+#undef LNF8
+  VJ_LAUNCH_CHECK("vj_layernorm_fwd_fp8");
+  return VJ_OK;
+}
+
+extern "C" int vj_quant_rows_fp8(int M, int K, const void* x, int x_bf16, long ldx, void* y8, long ldy, int* yexp,
+                                 void* stream) {
+  if (M == 0) return VJ_OK;
+  VJ_CHECK_ARG(K > 0 && K % 4 == 0 && ldx % 4 == 0 && ldy % 16 == 0 && ldy >= K && x && y8 && yexp,
+               "vj_quant_rows_fp8: K %% 4, ldy %% 16 and non-null operands required");
+  VJ_CHECK_ARG(!((uintptr_t)y8 & 15) && !((uintptr_t)x & 15), "vj_quant_rows_fp8: 16-B aligned rows");
+  const dim3 grid((M + 3) / 4);
+  if (x_bf16)
+    hipLaunchKernelGGL(k_quant_rows_fp8<true>, grid, dim3(256), 0, (hipStream_t)stream, M, K, x, ldx,
+                       (unsigned char*)y8, ldy, yexp);
+  else
+    hipLaunchKernelGGL(k_quant_rows_fp8<false>, grid, dim3(256), 0, (hipStream_t)stream, M, K, x, ldx,
+                       (unsigned char*)y8, ldy, yexp);
+  VJ_LAUNCH_CHECK("vj_quant_rows_fp8");
   return VJ_OK;
 }

@@ -51,6 +51,23 @@ def weight_bf16_t(p):
     return c[1]
 
 
+def weight_fp8(p):
+    """Per-output-channel scaled e4m3 copy of a Linear weight [out, in] (the fp8 target encoder's B
+    operands): (uint8 [out, in], int32 [out]), quantised from the fp32 master weight once per
+    weight update and cached."""
+    arena_owned = getattr(p, "_vj_bf16", None) is not None
+    key = (p.data_ptr(), SHADOW_EPOCH[0] if arena_owned else p._version)
+    c = getattr(p, "_vj_fp8", None)
+    if c is None or c[0] != key:
+        w = p.detach().reshape(p.shape[0], -1)
+        if not w.is_contiguous():
+            w = w.contiguous()
+        out = c[1] if c is not None else (None, None)
+        c = (key, ops.quant_rows_fp8(w, out=out[0], exps=out[1]))
+        p._vj_fp8 = c
+    return c[1]
+
+
 def grad_buf(p):
     if p.grad is None:
         p.grad = torch.zeros_like(p)
@@ -97,6 +114,29 @@ def _attn_scale(attn, hd):
     # F.scaled_dot_product_attention uses the default 1/sqrt(hd) (modules.py:367-372); the non-SDPA
     # branch uses attn.scale (= qk_scale or hd^-0.5).
     return hd**-0.5 if attn.use_sdpa else attn.scale
+
+
+def block_forward_fp8(x, blk, lay):
+    """Forward-only block with the QKV and fc1 GEMMs on the fp8 MFMA (opt-in for the no-grad target
+    encoder, BASELINE configs[4]): LN1 / LN2 write per-row scaled e4m3, the weights are per-channel
+    scaled e4m3; attention, proj and fc2 stay bf16 (their inputs come out of the attention / GELU
+    kernels, whose rows span many tiles). f32 residual stream as in block_forward."""
+    attn, mlp = blk.attn, blk.mlp
+    H = attn.num_heads
+    hd = x.shape[1] // H
+    ln1, e1 = ops.layernorm_fwd_fp8(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps)
+    w8, ew = weight_fp8(attn.qkv.weight)
+    if attn.use_rope:
+        c, s = rope_tables(hd, x.device, lay.npos)
+        qkv = ops.qkv_rope_fp8(ln1, e1, w8, ew, attn.qkv.bias, H, hd, lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
+    else:
+        qkv = ops.linear_fwd_fp8(ln1, e1, w8, ew, attn.qkv.bias, EPI_BF16)
+    o, _ = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd))
+    x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32_RESID, resid=x)
+    ln2, e2 = ops.layernorm_fwd_fp8(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
+    w18, ew1 = weight_fp8(mlp.fc1.weight)
+    _, act = ops.linear_fwd_fp8(ln2, e2, w18, ew1, mlp.fc1.bias, EPI_GELU)
+    return ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_F32_RESID, resid=x_mid)
 
 
 def block_forward(x, blk, lay, save):
@@ -198,9 +238,13 @@ def _needs_grad(x, mod):
         (x is not None and x.requires_grad) or any(p.requires_grad for p in mod.parameters()))
 
 
-def run_block(x, blk, lay):
+def run_block(x, blk, lay, fp8=False):
     if _needs_grad(x, blk):
+        if fp8:
+            raise NotImplementedError("the fp8 block path is forward-only (the no-grad target encoder)")
         return _BlockFn.apply(x, blk.norm1.weight, blk, lay)
+    if fp8:
+        return block_forward_fp8(x, blk, lay)
     return block_forward(x, blk, lay, save=False)[0]
 
 

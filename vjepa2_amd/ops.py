@@ -226,6 +226,65 @@ def layernorm_bwd(dy, x, mean, rstd, weight, dres_in=None, dweight=None, dbias=N
     return dres, dres_bf
 
 
+# ------------------------------------------------------------------------------------------------
+# fp8 (OCP e4m3) with per-row power-of-two scales: (bytes uint8 [M, K], exponents int32 [M])
+FP8 = torch.uint8
+
+
+def quant_rows_fp8(x, out=None, exps=None):
+    """Per-row scaled e4m3 of x f32 / bf16 [M, K] -> (uint8 [M, K], int32 [M])."""
+    _dev(x)
+    M, K = x.shape
+    out = out if out is not None else torch.empty(M, K, dtype=FP8, device=x.device)
+    exps = exps if exps is not None else torch.empty(M, dtype=torch.int32, device=x.device)
+    _call("vj_quant_rows_fp8", M, K, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(out), _rowmajor(out, "out"),
+          _p(exps), _stream())
+    return out, exps
+
+
+def layernorm_fwd_fp8(x, weight, bias, eps):
+    """LayerNorm with a per-row scaled e4m3 output -> (uint8 [M, D], int32 [M])."""
+    _dev(x)
+    M, D = x.shape
+    y = torch.empty(M, D, dtype=FP8, device=x.device)
+    e = torch.empty(M, dtype=torch.int32, device=x.device)
+    _call("vj_layernorm_fwd_fp8", M, D, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(weight), _p(bias),
+          float(eps), _p(y), D, _p(e), None, None, _stream())
+    return y, e
+
+
+def linear_fwd_fp8(x8, ex, w8, ew, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
+    """Y = (x8 * 2^ex) (w8 * 2^ew)^T + b on the fp8 MFMA; epilogues as linear_fwd."""
+    _dev(x8, w8, bias, resid)
+    assert x8.dtype == FP8 and w8.dtype == FP8 and ex.dtype == torch.int32 and ew.dtype == torch.int32
+    M, K = x8.shape
+    N = w8.shape[0]
+    assert w8.shape[1] == K
+    if epi == EPI_BF16:
+        out = out if out is not None else torch.empty(M, N, dtype=BF16, device=x8.device)
+    elif epi in (EPI_F32, EPI_F32_RESID):
+        out = out if out is not None else torch.empty(M, N, dtype=F32, device=x8.device)
+    elif epi == EPI_GELU:
+        out2 = out2 if out2 is not None else torch.empty(M, N, dtype=BF16, device=x8.device)
+    _call("vj_gemm_fp8", M, N, K, _p(x8), _rowmajor(x8, "x8"), _p(ex), _p(w8), _rowmajor(w8, "w8"), _p(ew), epi,
+          _p(bias), _p(resid), resid.stride(0) if resid is not None else 0, _p(out),
+          out.stride(0) if out is not None else 0, _p(out2), out2.stride(0) if out2 is not None else 0, _stream(),
+          label=f"k_gemm_fp8<{EPI_NAMES[epi]}>", flops=2.0 * M * N * K)
+    return (out, out2) if epi == EPI_GELU else out
+
+
+def qkv_rope_fp8(x8, ex, w8, ew, bias, H, hd, ids, ids_mod, tpf, tpr, cos_tab, sin_tab):
+    _dev(x8, w8, bias, ids, cos_tab, sin_tab)
+    M, K = x8.shape
+    N = 3 * H * hd
+    assert w8.shape == (N, K) and x8.dtype == FP8 and w8.dtype == FP8
+    out = torch.empty(M, N, dtype=BF16, device=x8.device)
+    _call("vj_qkv_rope_gemm_fp8", M, K, _p(x8), _rowmajor(x8, "x8"), _p(ex), _p(w8), _rowmajor(w8, "w8"), _p(ew),
+          _p(bias), _p(out), N, H, hd, _p(ids), int(ids_mod), int(tpf), int(tpr), _p(cos_tab), _p(sin_tab),
+          cos_tab.shape[0], _stream(), label="k_gemm_fp8<EPI_ROPE>", flops=2.0 * M * N * K)
+    return out
+
+
 def rope_(qkv, H, hd, q_off, k_off, ids, ids_mod, tpf, tpr, cos_tab, sin_tab, inverse=False):
     _dev(qkv, ids, cos_tab, sin_tab)
     T = qkv.shape[0]

@@ -110,13 +110,15 @@ class JEPATrainer:
     """The fused V-JEPA train step (app/vjepa/train.py:409-471) over arena-owned parameters."""
 
     def __init__(self, encoder, predictor, target_encoder, optimizer, mixed_precision=True, loss_exp=1.0, world_size=1,
-                 bucket_mb=64, group=None):
+                 bucket_mb=64, group=None, fp8_target=False):
         unwrap = lambda m: getattr(m, "backbone", getattr(m, "module", m))  # noqa: E731
         self.enc, self.pred, self.tgt = unwrap(encoder), unwrap(predictor), unwrap(target_encoder)
         self.opt = optimizer
         self.mixed_precision = mixed_precision
         self.loss_exp = loss_exp
         self.world = world_size
+        # opt-in: the no-grad target encoder's QKV / fc1 GEMMs on the fp8 MFMA (functions.block_forward_fp8)
+        self.fp8_target = fp8_target
         enc_w, pred_w, enc_n, pred_n = optimizer.arenas
         device = enc_w.data.device
         tnamed = dict(target_encoder.named_parameters())
@@ -151,10 +153,10 @@ class JEPATrainer:
             main = torch.cuda.current_stream()
             side.wait_stream(main)  # clips + this step's EMA'd target weights are ready
             with torch.cuda.stream(side), torch.no_grad():
-                h = self.tgt.forward_features(clips)
+                h = self.tgt.forward_features(clips, fp8=self.fp8_target)
         else:
             with torch.no_grad():
-                h = self.tgt.forward_features(clips)
+                h = self.tgt.forward_features(clips, fp8=self.fp8_target)
         z, _ = self.enc.forward_ragged(clips, masks_enc, out_dtype=torch.bfloat16)
         zp, pl = self.pred.forward_ragged(z, masks_enc, masks_pred, mask_index=mask_index, out_dtype=torch.bfloat16)
         if side is not None:
@@ -360,8 +362,9 @@ def main(args, resume_preempt=False):
         encoder=encoder, predictor=predictor, wd=wd, final_wd=final_wd, start_lr=start_lr, ref_lr=lr,
         final_lr=final_lr, iterations_per_epoch=ipe, warmup=warmup, num_epochs=num_epochs, ipe_scale=ipe_scale,
         mixed_precision=mixed_precision, betas=betas, eps=eps)
+    # meta.fp8_target (this build's opt-in key; the reference has no fp8 and ignores unknown keys)
     trainer = JEPATrainer(encoder, predictor, target_encoder, optimizer, mixed_precision=mixed_precision,
-                          loss_exp=loss_exp, world_size=world_size)
+                          loss_exp=loss_exp, world_size=world_size, fp8_target=bool(cfgs_meta.get("fp8_target", False)))
     momentum_scheduler = (ema[0] + i * (ema[1] - ema[0]) / (ipe * num_epochs * ipe_scale)
                           for i in range(int(ipe * num_epochs * ipe_scale) + 1))
     start_epoch = 0

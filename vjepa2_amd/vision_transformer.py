@@ -154,20 +154,21 @@ class VisionTransformer(nn.Module):
         t = fn.run_patch_embed(x, self.patch_embed, masks, pos_table=pos, pos_ids=lay.ids, pos_mod=N)
         return t, lay
 
-    def forward_ragged(self, x, masks, out_dtype=torch.bfloat16, final_norm=True):
-        """All masks in ONE pass. Returns (tokens [sum_m B*K_m, D], layout)."""
+    def forward_ragged(self, x, masks, out_dtype=torch.bfloat16, final_norm=True, fp8=False):
+        """All masks in ONE pass. Returns (tokens [sum_m B*K_m, D], layout). fp8: QKV / fc1 GEMMs on
+        the fp8 MFMA (forward-only, functions.block_forward_fp8)."""
         t, lay = self.tokens(x, masks)
         for blk in self.blocks:
-            t = fn.run_block(t, blk, lay)
+            t = fn.run_block(t, blk, lay, fp8=fp8)
         if final_norm:
             t = fn.run_layernorm(t, self.norm, out_dtype=out_dtype)
         return t, lay
 
     @torch.no_grad()
-    def forward_features(self, x):
+    def forward_features(self, x, fp8=False):
         """All tokens, no final norm (f32 residual stream [B*N, D]); used by the target encoder,
         whose final norm is fused into the JEPA loss kernel."""
-        t, _ = self.forward_ragged(x, None, final_norm=False)
+        t, _ = self.forward_ragged(x, None, final_norm=False, fp8=fp8)
         return t
 
     def forward(self, x, masks=None):

@@ -41,6 +41,8 @@ GEMMS = [
     ("fc1  tgt", 49152, 4096, 1024, 1, 1, 3, 1),
     ("qkv  tgt", 49152, 3072, 1024, 1, 1, 0, 1),
     ("proj tgt", 49152, 1024, 1024, 1, 1, 2, 1),
+    ("proj tgt f32", 49152, 1024, 1024, 1, 1, 1, 1),
+    ("proj tgt bf16", 49152, 1024, 1024, 1, 1, 0, 1),
     ("fc2  tgt", 49152, 1024, 4096, 1, 1, 2, 1),
     ("fc2  tgt bf16", 49152, 1024, 4096, 1, 1, 0, 1),
     ("dgrad fc2 Wt", 11712, 4096, 1024, 1, 1, 0, 1),

@@ -8,7 +8,7 @@ import sys
 
 def main(d):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")[:60]
             acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))

@@ -170,7 +170,9 @@ def _attn_ref(q, k, v, groups, scale):
 @pytest.mark.parametrize("hd,H,groups", [(64, 2, [(3, 70), (2, 130)]), (32, 3, [(2, 257), (1, 5)]),
                                          (64, 1, [(1, 128)]), (32, 2, [(4, 33)]),
                                          # vit_huge / vit_giant head dims (padded to 96 inside)
-                                         (80, 2, [(2, 150), (1, 33)]), (88, 2, [(1, 200), (3, 31)])])
+                                         (80, 2, [(2, 150), (1, 33)]), (88, 2, [(1, 200), (3, 31)]),
+                                         # long sequences: ViT-L 16x256^2 (2048), ViT-g 16x384^2 (4608)
+                                         (64, 2, [(1, 2048), (1, 4608)]), (32, 2, [(1, 4608), (1, 1504)])])
 def test_attention_fwd_bwd(hd, H, groups):
     from vjepa2_amd import ops
 

@@ -67,7 +67,12 @@ ATTN = [("attn fwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], False),
         ("attn fwd hd64 tgt", 64, 16, [(24, 2048)], False),
         ("attn bwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], True),
         ("attn fwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], False),
-        ("attn bwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], True)]
+        ("attn bwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], True),
+        ("attn fwd hd64 N2048", 64, 16, [(8, 2048)], False),
+        ("attn bwd hd64 N2048", 64, 16, [(8, 2048)], True),
+        ("attn bwd hd64 N4608", 64, 16, [(2, 4608)], True),
+        ("attn bwd hd32 N4608", 32, 12, [(4, 4608)], True),
+        ("attn fwd hd64 N8192", 64, 22, [(2, 8192)], False)]
 
 
 def gemm_case(lib, case, dev, stream):
@@ -116,7 +121,7 @@ def attn_case(lib, hd, H, groups, dev, stream, bwd):
         assert lib.vj_attn_bwd(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(do), D, P(stats), P(dqkv), 3 * D, sc,
                                len(groups), ns, ln, None, 0, 0, 0, None, None, stream) == 0
     fl = sum(4.0 * n * l * l * D for n, l in groups)
-    return (bwdf, 2 * fl) if bwd else (fwd, fl)
+    return (bwdf, 2.5 * fl) if bwd else (fwd, fl)  # backward: FA2 convention, 5 matmuls
 
 
 def time_fn(fn, iters=10):

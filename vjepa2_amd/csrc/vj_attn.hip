@@ -38,6 +38,11 @@
 #define VJ_ATTN_QW64 1
 #endif
 
+// forward workgroups per CU the register budget is sized for (head dims <= 64)
+#ifndef VJ_ATTN_FWD_OCC
+#define VJ_ATTN_FWD_OCC 3
+#endif
+
 namespace {
 
 constexpr int MAXG = 4;
@@ -227,7 +232,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 // ------------------------------------------------------------------------------------------------
 // Forward: block = 4 waves x 32 queries, KV tiles of 64 keys double-buffered in LDS.
 template <int HD>
-__global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
+__global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_fwd(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr int KT = 64;
   constexpr int TB = KT * HDP * 2;  // bytes per K or V tile
@@ -253,18 +258,14 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
   const __amdgpu_buffer_rsrc_t rk = make_rsrc(kbase, bytes);
   const __amdgpu_buffer_rsrc_t rv = make_rsrc(vbase, bytes);
 
-  // O^T accumulators; lt = "ones row" tile: row 0 of V^T replaced by ones gives l = sum_k p (the
-  // softmax denominator of the same bf16 P the numerator uses) on the MFMA pipe instead of 32 adds.
-  f32x16 ot[HDP / 32], lt;
+  // O^T accumulators; lsum = this lane's share of l = sum_k p (its 16 key rows of each 32-key
+  // half; lanes q and q + 32 together hold query q's keys), summed on the VALU in f32
+  f32x16 ot[HDP / 32];
+  float lsum = 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < 16; ++r)
 #pragma unroll
     for (int d = 0; d < HDP / 32; ++d) ot[d][r] = 0.f;
-    lt[r] = 0.f;
-  }
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)((lane & 31) == 0 ? 1.f : 0.f);
   // Lazy rescaling: p = exp2(c*s - c*m_use) with m_use the raw-score max seen when O was last
   // rescaled; O is rescaled (wave-uniform branch) only when some query's max grows by more than
   // TAU/c, so p <= 2^TAU stays well inside fp32/bf16 range. The result is invariant to m_use.
@@ -332,16 +333,23 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
       m_use = m_new;
       cm = m_new * c;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+      for (int r = 0; r < 16; ++r)
 #pragma unroll
         for (int d = 0; d < HDP / 32; ++d) ot[d][r] *= alpha;
-        lt[r] *= alpha;
-      }
+      lsum *= alpha;
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[kk][r] = __builtin_amdgcn_exp2f(fmaf(st[kk][r], c, -cm));
+    // two partial chains keep the adds off one dependency path
+    float ls0 = st[0][0], ls1 = st[1][0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      ls0 += st[0][r];
+      ls1 += st[1][r];
+    }
+    lsum += ls0 + ls1;
     // O^T += V^T P^T over 4 key-steps of 16
     lds_wait();
 #pragma unroll
@@ -351,7 +359,6 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
       const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
 #pragma unroll
       for (int d = 0; d < HDP / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
-      lt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf, lt, 0, 0, 0);
     }
     __syncthreads();
   };
@@ -359,7 +366,7 @@ __global__ __launch_bounds__(256) void k_attn_fwd(AttnArgs a) {
     tile_iter(kt0, std::integral_constant<int, 0>{});
     if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
   }
-  const float l_tot = __shfl(lt[0], lane & 31, 64);  // row 0 of the ones tile lives in lanes 0..31
+  const float l_tot = lsum + __shfl_xor(lsum, 32, 64);
   const float inv = 1.f / l_tot;
   if (qok) {
     bf16_t* orow = a.o + (long)(seq0 + qloc) * a.ldo + h * HD;

@@ -323,7 +323,7 @@ def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None):
     _call("vj_attn_bwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
           _rowmajor(do, "do"), _p(stats), _p(dqkv), _rowmajor(dqkv, "dqkv"), float(scale), len(groups), int_array(ns),
           int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), _stream(), label=f"attn_bwd<hd{hd}>",
-          flops=sum(8.0 * n * l * l * D for n, l in groups))
+          flops=sum(10.0 * n * l * l * D for n, l in groups))  # FA2 convention: 5 matmuls = 2.5 x forward
     return dqkv
 
 

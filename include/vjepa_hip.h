@@ -161,6 +161,23 @@ int vj_cast_bf16(long n, const float* in, void* out, void* stream);
  * data-gradient GEMM dX = dY W (nn.Linear backward) reads as its B operand. */
 int vj_transpose_bf16(int rows, int cols, const void* src, long ld_src, void* dst, long ld_dst, void* stream);
 
+/* fp32-operand parity mode (vj_f32.hip): the encoder forward with f32 operands throughout, to show
+ * the bf16 path's distance from the fp32 reference is operand rounding only. Not on the training
+ * path. vj_gemm_f32: C = A B^T + bias (+ resid), epi as vj_gemm_bf16 (F32 = 1, F32_RESID = 2,
+ * GELU = 3: C = pre-activation, C2 = GELU) on v_mfma_f32_32x32x2_f32 (replaces the f32 math of
+ * nn.Linear, modules.py:77-83 / 330 / 372). vj_attn_fwd_f32: exact-softmax attention on an f32 qkv
+ * buffer (F.scaled_dot_product_attention, modules.py:367-372); lse in natural log. vj_rope_f32 /
+ * vj_im2col_tubelet_f32: vj_rope / vj_im2col_tubelet on f32 rows. */
+int vj_gemm_f32(int M, int N, int K, const float* A, long lda, const float* B, long ldb, int epi, const float* bias,
+                const float* resid, long ldr, float* C, long ldc, float* C2, long ldc2, void* stream);
+int vj_attn_fwd_f32(int T, int H, int hd, const float* qkv, long ld, int q_off, int k_off, int v_off, float* o,
+                    long ldo, float* lse, float scale, int ngroups, const int* nseq, const int* len, void* stream);
+int vj_rope_f32(int T, int H, int hd, float* qkv, long ld, int q_off, int k_off, const int* ids, int ids_mod,
+                int tokens_per_frame, int tokens_per_row, const float* cos_tab, const float* sin_tab, int half,
+                void* stream);
+int vj_im2col_tubelet_f32(int R, int K, const long* idx, int B, int C, int Tf, int Hf, int Wf, int tub, int pch,
+                          const float* clip, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

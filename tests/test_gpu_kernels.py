@@ -198,6 +198,46 @@ def test_attention_fwd_bwd(hd, H, groups):
     assert torch.equal(dqkv, dqkv2)
 
 
+@pytest.mark.parametrize("M,N,K,epi", [(300, 520, 1024, 1), (1100, 384, 200, 2), (64, 4096, 1024, 3), (5, 8, 3, 1)])
+def test_gemm_f32_parity_mode(M, N, K, epi):
+    """fp32-operand parity mode GEMM (v_mfma_f32_32x32x2_f32) vs fp64 math: f32 accumulation only."""
+    from vjepa2_amd import ops
+
+    g = torch.Generator().manual_seed(M + N + K)
+    a, w, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) / K ** 0.5, torch.randn(N, generator=g)
+    r = torch.randn(M, N, generator=g)
+    exp = a.double() @ w.double().t() + b.double()
+    bound = 4 * K * 2.0 ** -24 * (a.double().abs() @ w.double().abs().t() + b.double().abs())
+    out = ops.linear_fwd_f32(a.to(DEV), w.to(DEV), b.to(DEV), epi, resid=r.to(DEV) if epi == 2 else None)
+    torch.cuda.synchronize()
+    if epi == 2:
+        exp = exp + r.double()
+        bound = bound + 2.0 ** -23 * exp.abs()
+    if epi == 3:
+        pre, act = out
+        assert ((pre.cpu().double() - exp).abs() <= bound).all()
+        ga = torch.nn.functional.gelu(pre.cpu().double())
+        assert (act.cpu().double() - ga).abs().max().item() <= 1e-6 * max(1.0, ga.abs().max().item())
+    else:
+        assert ((out.cpu().double() - exp).abs() <= bound).all()
+
+
+@pytest.mark.parametrize("hd,H,groups", [(64, 2, [(2, 300), (1, 77)]), (32, 3, [(1, 1504)]), (88, 1, [(2, 130)])])
+def test_attention_f32_parity_mode(hd, H, groups):
+    """fp32-operand parity mode attention vs fp32 torch softmax attention (ulp-level)."""
+    from vjepa2_amd import ops
+
+    T = sum(n * l for n, l in groups)
+    D = H * hd
+    qkv = torch.randn(T, 3 * D, generator=torch.Generator().manual_seed(hd + T))
+    o, lse = ops.attn_fwd_f32(qkv.to(DEV), H, hd, groups, hd ** -0.5)
+    q, k, v = (qkv[:, i * D:(i + 1) * D].double().reshape(T, H, hd) for i in range(3))
+    o_ref, lse_ref = _attn_ref(q, k, v, groups, hd ** -0.5)
+    torch.cuda.synchronize()
+    _close(o.reshape(T, H, hd), o_ref, 2e-6, 2e-5, f"attn f32 hd={hd}")
+    _close(lse, lse_ref, 2e-6, 2e-6, f"attn f32 lse hd={hd}")
+
+
 @pytest.mark.parametrize("hd", [64, 32, 80])
 def test_attention_rescale_spikes(hd):
     """Score maxima that grow tile after tile (every step takes the lazy-rescale branch) and one

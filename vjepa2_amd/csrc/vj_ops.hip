@@ -301,7 +301,8 @@ __global__ __launch_bounds__(1024) void k_colsum2(int S, int N, const float* __r
 // angle theta_{j mod sw/2}; partner y_{2i} = -x_{2i+1}, y_{2i+1} = x_{2i} (modules.py:43-50).
 // Angles come from host-built tables cos/sin[pos][i] (computed with the reference's fp32 ops).
 // Thread = one 8-element chunk of one head of q or k.
-__global__ void k_rope(int T, int H, int hd, bf16_t* __restrict__ qkv, long ld, int q_off, int k_off,
+template <bool F32>
+__global__ void k_rope(int T, int H, int hd, void* __restrict__ qkv_, long ld, int q_off, int k_off,
                        const int* __restrict__ ids, int ids_mod, int tpf, int tpr, const float* __restrict__ ctab,
                        const float* __restrict__ stab, int half, int inverse) {
   const int cpr = hd / 8;
@@ -321,13 +322,18 @@ __global__ void k_rope(int T, int H, int hd, bf16_t* __restrict__ qkv, long ld, 
   const int fr = id / tpf;
   const int hr = (id - tpf * fr) / tpr;
   const int wc = (id - tpf * fr) - tpr * hr;
-  bf16_t* p = qkv + t * ld + (which ? k_off : q_off) + h * hd + e0;
-  uint4 u = *(uint4*)p;
-  bf16_t v[8];
-  *(uint4*)v = u;
+  const long off = t * ld + (which ? k_off : q_off) + h * hd + e0;
   float x[8], o[8];
+  if constexpr (F32) {  // fp32-operand parity mode
+    const float4* p = (const float4*)((float*)qkv_ + off);
+    const float4 a = p[0], b = p[1];
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+  } else {
+    bf16_t v[8];
+    *(uint4*)v = *(const uint4*)((bf16_t*)qkv_ + off);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = bf2f(v[j]);
+    for (int j = 0; j < 8; ++j) x[j] = bf2f(v[j]);
+  }
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {
     const int e = e0 + j;  // even element index within the head
@@ -350,17 +356,25 @@ __global__ void k_rope(int T, int H, int hd, bf16_t* __restrict__ qkv, long ld, 
       o[j + 1] = -x[j] * s0 + x[j + 1] * c1;
     }
   }
+  if constexpr (F32) {
+    float4* p = (float4*)((float*)qkv_ + off);
+    p[0] = make_float4(o[0], o[1], o[2], o[3]);
+    p[1] = make_float4(o[4], o[5], o[6], o[7]);
+  } else {
+    bf16_t v[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = f2bf(o[j]);
-  *(uint4*)p = *(uint4*)v;
+    for (int j = 0; j < 8; ++j) v[j] = f2bf(o[j]);
+    *(uint4*)((bf16_t*)qkv_ + off) = *(uint4*)v;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
 // Tubelet im2col (Conv3d k = s = (tub, p, p) as a GEMM operand), gathering only the listed tokens.
 // clip f32 [B, C, Tf, Hf, Wf]; row r -> (b, token) with token = idx ? idx[r] : r % N, b = r / K.
 // out bf16 [R, C*tub*p*p], column = c*tub*p*p + kt*p*p + kh*p + kw (= Conv3d weight flattening).
+template <bool F32>
 __global__ void k_im2col(int R, int K, const long* __restrict__ idx, int C, int Tf, int Hf, int Wf, int tub,
-                         int pch, const float* __restrict__ clip, bf16_t* __restrict__ out) {
+                         int pch, const float* __restrict__ clip, void* __restrict__ out) {
   const int r = blockIdx.x;
   if (r >= R) return;
   const int b = r / K;
@@ -378,7 +392,8 @@ __global__ void k_im2col(int R, int K, const long* __restrict__ idx, int C, int 
     const int c = col / (pch * pch * tub);
     const float* src = clip + ((((long)b * C + c) * Tf + (tt * tub + kt)) * Hf + (hh * pch + kh)) * Wf + ww * pch + kw;
     const float4 v = *(const float4*)src;
-    *(uint2*)(out + (long)r * kdim + col) = make_uint2(pack_bf2(v.x, v.y), pack_bf2(v.z, v.w));
+    if constexpr (F32) *(float4*)((float*)out + (long)r * kdim + col) = v;  // fp32-operand parity mode
+    else *(uint2*)((bf16_t*)out + (long)r * kdim + col) = make_uint2(pack_bf2(v.x, v.y), pack_bf2(v.z, v.w));
   }
 }
 
@@ -814,10 +829,26 @@ extern "C" int vj_rope(int T, int H, int hd, void* qkv, long ld, int q_off, int 
   VJ_CHECK_ARG(half == (hd / 3) / 2 && half >= 1, "vj_rope: half=%d inconsistent with hd=%d", half, hd);
   VJ_CHECK_ARG(ids || ids_mod > 0, "vj_rope: ids or ids_mod required");
   const long total = (long)T * 2 * H * (hd / 8);
-  hipLaunchKernelGGL(k_rope, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, T, H, hd,
-                     (bf16_t*)qkv, ld, q_off, k_off, ids, ids_mod, tokens_per_frame, tokens_per_row, cos_tab, sin_tab,
-                     half, inverse);
+  hipLaunchKernelGGL(k_rope<false>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, T, H,
+                     hd, qkv, ld, q_off, k_off, ids, ids_mod, tokens_per_frame, tokens_per_row, cos_tab, sin_tab, half,
+                     inverse);
   VJ_LAUNCH_CHECK("vj_rope");
+  return VJ_OK;
+}
+
+// vj_rope on an f32 qkv buffer (fp32-operand parity mode); same arguments, ld / offsets in floats.
+extern "C" int vj_rope_f32(int T, int H, int hd, float* qkv, long ld, int q_off, int k_off, const int* ids,
+                           int ids_mod, int tokens_per_frame, int tokens_per_row, const float* cos_tab,
+                           const float* sin_tab, int half, void* stream) {
+  if (T == 0) return VJ_OK;
+  VJ_CHECK_ARG(hd % 8 == 0 && ld % 4 == 0 && q_off % 4 == 0 && k_off % 4 == 0, "vj_rope_f32: alignment");
+  VJ_CHECK_ARG(half == (hd / 3) / 2 && half >= 1, "vj_rope_f32: half=%d inconsistent with hd=%d", half, hd);
+  VJ_CHECK_ARG(ids || ids_mod > 0, "vj_rope_f32: ids or ids_mod required");
+  const long total = (long)T * 2 * H * (hd / 8);
+  hipLaunchKernelGGL(k_rope<true>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, T, H,
+                     hd, (void*)qkv, ld, q_off, k_off, ids, ids_mod, tokens_per_frame, tokens_per_row, cos_tab,
+                     sin_tab, half, 0);
+  VJ_LAUNCH_CHECK("vj_rope_f32");
   return VJ_OK;
 }
 
@@ -826,9 +857,21 @@ extern "C" int vj_im2col_tubelet(int R, int K, const long* idx, int B, int C, in
   if (R == 0) return VJ_OK;
   VJ_CHECK_ARG(pch % 4 == 0 && Tf % tub == 0 && Hf % pch == 0 && Wf % pch == 0, "vj_im2col_tubelet: bad geometry");
   VJ_CHECK_ARG(R <= (long)B * K, "vj_im2col_tubelet: R=%d > B*K", R);
-  hipLaunchKernelGGL(k_im2col, dim3(R), dim3(256), 0, (hipStream_t)stream, R, K, idx, C, Tf, Hf, Wf, tub, pch, clip,
-                     (bf16_t*)out);
+  hipLaunchKernelGGL(k_im2col<false>, dim3(R), dim3(256), 0, (hipStream_t)stream, R, K, idx, C, Tf, Hf, Wf, tub, pch,
+                     clip, out);
   VJ_LAUNCH_CHECK("vj_im2col_tubelet");
+  return VJ_OK;
+}
+
+// vj_im2col_tubelet with f32 rows (fp32-operand parity mode)
+extern "C" int vj_im2col_tubelet_f32(int R, int K, const long* idx, int B, int C, int Tf, int Hf, int Wf, int tub,
+                                     int pch, const float* clip, float* out, void* stream) {
+  if (R == 0) return VJ_OK;
+  VJ_CHECK_ARG(pch % 4 == 0 && Tf % tub == 0 && Hf % pch == 0 && Wf % pch == 0, "vj_im2col_tubelet_f32: bad geometry");
+  VJ_CHECK_ARG(R <= (long)B * K, "vj_im2col_tubelet_f32: R=%d > B*K", R);
+  hipLaunchKernelGGL(k_im2col<true>, dim3(R), dim3(256), 0, (hipStream_t)stream, R, K, idx, C, Tf, Hf, Wf, tub, pch,
+                     clip, (void*)out);
+  VJ_LAUNCH_CHECK("vj_im2col_tubelet_f32");
   return VJ_OK;
 }
 

@@ -162,6 +162,38 @@ def block_forward(x, blk, lay, save):
     return x_out, saved
 
 
+def block_forward_f32(x, blk, lay):
+    """fp32-operand parity mode of block_forward: the same LayerNorm / RoPE kernels, f32 MFMA GEMMs
+    (vj_gemm_f32) and exact-softmax attention (vj_attn_fwd_f32); every intermediate stays f32."""
+    attn, mlp = blk.attn, blk.mlp
+    H = attn.num_heads
+    hd = x.shape[1] // H
+    ln1, _, _ = ops.layernorm_fwd(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, out_dtype=F32, want_stats=False)
+    qkv = ops.linear_fwd_f32(ln1, attn.qkv.weight.detach().float(), attn.qkv.bias, EPI_F32)
+    if attn.use_rope:
+        c, s = rope_tables(hd, x.device, lay.npos)
+        ops.rope_f32_(qkv, H, hd, lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
+    o, _ = ops.attn_fwd_f32(qkv, H, hd, lay.groups, _attn_scale(attn, hd))
+    x_mid = ops.linear_fwd_f32(o, attn.proj.weight.detach().float(), attn.proj.bias, EPI_F32_RESID, resid=x)
+    ln2, _, _ = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, out_dtype=F32,
+                                  want_stats=False)
+    _, act = ops.linear_fwd_f32(ln2, mlp.fc1.weight.detach().float(), mlp.fc1.bias, EPI_GELU)
+    return ops.linear_fwd_f32(act, mlp.fc2.weight.detach().float(), mlp.fc2.bias, EPI_F32_RESID, resid=x_mid)
+
+
+def patch_embed_forward_f32(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0):
+    """fp32-operand parity mode of patch_embed_forward."""
+    proj = pe.proj
+    D = proj.weight.shape[0]
+    p, tub = pe.patch_size, pe.tubelet_size
+    cols = ops.im2col_f32(clip, p, tub) if masks is None else torch.cat(
+        [ops.im2col_f32(clip, p, tub, idx=m.contiguous()) for m in masks], 0)
+    x = ops.linear_fwd_f32(cols, proj.weight.detach().float().reshape(D, -1).contiguous(), proj.bias, EPI_F32)
+    if pos_table is not None:
+        ops.add_rows(x, pos_table, idx=pos_ids, idx_mod=pos_mod)
+    return x
+
+
 def _bias_buf(lin):
     return grad_buf(lin.bias) if lin.bias is not None and lin.bias.requires_grad else None
 

@@ -459,3 +459,61 @@ def cast_bf16(x, out=None):
     out = out if out is not None else torch.empty(x.shape, dtype=BF16, device=x.device)
     _call("vj_cast_bf16", x.numel(), _p(x), _p(out), _stream())
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# fp32-operand parity mode (vj_f32.hip): f32 operands throughout, off the training path.
+
+
+def linear_fwd_f32(x, w, bias=None, epi=EPI_F32, resid=None):
+    """Y = X W^T + b on the f32 MFMA; x f32 [M, K], w f32 [N, K]. EPI_GELU -> (pre, act)."""
+    _dev(x, w, bias, resid)
+    assert x.dtype == F32 and w.dtype == F32
+    M, K = x.shape
+    N = w.shape[0]
+    assert w.shape[1] == K
+    y = torch.empty(M, N, dtype=F32, device=x.device)
+    y2 = torch.empty(M, N, dtype=F32, device=x.device) if epi == EPI_GELU else None
+    if epi == EPI_F32_RESID:
+        assert resid is not None and resid.dtype == F32 and resid.shape == (M, N)
+    _call("vj_gemm_f32", M, N, K, _p(x), _rowmajor(x, "x"), _p(w), _rowmajor(w, "w"), epi, _p(bias), _p(resid),
+          resid.stride(0) if resid is not None else 0, _p(y), N, _p(y2), N if y2 is not None else 0, _stream(),
+          label="k_gemm_f32", flops=2.0 * M * N * K)
+    return (y, y2) if epi == EPI_GELU else y
+
+
+def attn_fwd_f32(qkv, H, hd, groups, scale):
+    """Exact-softmax attention on f32 qkv [T, 3*H*hd] -> (O f32 [T, H*hd], lse f32 [H, T] natural log)."""
+    _dev(qkv)
+    assert qkv.dtype == F32
+    T = qkv.shape[0]
+    D = H * hd
+    o = torch.empty(T, D, dtype=F32, device=qkv.device)
+    lse = torch.empty(H, T, dtype=F32, device=qkv.device)
+    ns, ln = [g[0] for g in groups], [g[1] for g in groups]
+    _call("vj_attn_fwd_f32", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), D, _p(lse), float(scale),
+          len(groups), int_array(ns), int_array(ln), _stream())
+    return o, lse
+
+
+def rope_f32_(qkv, H, hd, ids, ids_mod, tpf, tpr, cos_tab, sin_tab):
+    """In-place 3-axis RoPE of the q and k columns of an f32 qkv buffer."""
+    _dev(qkv, ids, cos_tab, sin_tab)
+    assert qkv.dtype == F32
+    T = qkv.shape[0]
+    _call("vj_rope_f32", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, H * hd, _p(ids), int(ids_mod), int(tpf),
+          int(tpr), _p(cos_tab), _p(sin_tab), (hd // 3) // 2, _stream())
+
+
+def im2col_f32(clip, patch, tub, idx=None):
+    """im2col with f32 rows: clip f32 [B,C,T,H,W] -> f32 [B*K, C*tub*p*p]."""
+    _dev(clip, idx)
+    assert clip.dtype == F32 and clip.is_contiguous()
+    B, C, Tf, Hf, Wf = clip.shape
+    N = (Tf // tub) * (Hf // patch) * (Wf // patch)
+    K = idx.shape[1] if idx is not None else N
+    if idx is not None:
+        assert idx.dtype == torch.int64 and idx.is_contiguous() and idx.shape[0] == B and int(K) <= N
+    out = torch.empty(B * K, C * tub * patch * patch, dtype=F32, device=clip.device)
+    _call("vj_im2col_tubelet_f32", B * K, K, _p(idx), B, C, Tf, Hf, Wf, tub, patch, _p(clip), _p(out), _stream())
+    return out

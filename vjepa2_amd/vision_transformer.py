@@ -187,6 +187,33 @@ class VisionTransformer(nn.Module):
             t = fn.run_layernorm(t, self.norm)
         return self._reshape(t, lay)
 
+    @torch.no_grad()
+    def forward_fp32(self, x, masks=None):
+        """fp32-operand parity mode of forward(): f32 operands and intermediates throughout (f32 MFMA
+        GEMMs, exact-softmax attention, the same LayerNorm / RoPE kernels). Not a training path: it
+        isolates the bf16 path's operand rounding in the comparison with the fp32 reference."""
+        if masks is not None and not isinstance(masks, list):
+            masks = [masks]
+        x = x.float().contiguous()
+        B, Tp, Hp, Wp, tpf, tpr = self._geometry(x)
+        N = Tp * Hp * Wp
+        if masks is None:
+            lay = fn.TokenLayout([(B, N)], ids=None, ids_mod=N, tpf=tpf, tpr=tpr)
+        else:
+            masks = [m.to(device=x.device, dtype=torch.int64).contiguous() for m in masks]
+            lay = fn.TokenLayout([(B, m.shape[1]) for m in masks], ids=ops.ids_to_int32(masks), ids_mod=N,
+                                 tpf=tpf, tpr=tpr)
+        pos = None
+        if self.pos_embed is not None:
+            pos = self.interpolate_pos_encoding(x, self.pos_embed)[0].float().contiguous()
+        t = fn.patch_embed_forward_f32(x, self.patch_embed, masks, pos_table=pos, pos_ids=lay.ids, pos_mod=N)
+        for blk in self.blocks:
+            t = fn.block_forward_f32(t, blk, lay)
+        if self.norm is not None:
+            t, _, _ = ops.layernorm_fwd(t, self.norm.weight, self.norm.bias, self.norm.eps, out_dtype=torch.float32,
+                                        want_stats=False)
+        return self._reshape(t, lay)
+
     @staticmethod
     def _reshape(t, lay):
         lens = {l for _, l in lay.groups}

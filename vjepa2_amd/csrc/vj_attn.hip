@@ -132,6 +132,21 @@ __device__ __forceinline__ void rope_inv_rows(const AttnArgs& a, const TokPos& t
     }
 }
 
+// XCD-aware block order. The dispatcher sends linear block b (x fastest) to XCD b % 8; each XCD is
+// handed a contiguous range of the (head, tile) space instead, so the query / key tiles of one
+// (sequence, head) run on one XCD and re-read that sequence's K / V (forward, dQ) or Q / dO (dK/dV)
+// from its L2. Measured before: every XCD fetched every sequence's K / V, ~3x the qkv bytes per
+// launch from HBM (rocprofv3 FETCH_SIZE, profiles/r02_pmc_bench.txt).
+__device__ __forceinline__ void xcd_tile(int& tile, int& head) {
+  const int nx = gridDim.x;
+  const int total = nx * gridDim.y;
+  const int b = blockIdx.y * nx + blockIdx.x;
+  const int per = total >> 3, rem = total & 7, x = b & 7;
+  const int id = x * per + min(x, rem) + (b >> 3);
+  head = id / nx;
+  tile = id - head * nx;
+}
+
 // Locate (sequence start, length, tile index in sequence) of a flat tile id.
 __device__ __forceinline__ void locate(const SeqGroups& sg, int tile, int tiles_per_seq_div, int& seq_start,
                                        int& len, int& t_in_seq) {
@@ -239,9 +254,10 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = blockIdx.y;
+  int tile_id, h;
+  xcd_tile(tile_id, h);
   int seq0, len, qt;
-  locate(a.sg, blockIdx.x, 128, seq0, len, qt);
+  locate(a.sg, tile_id, 128, seq0, len, qt);
   const int qloc = qt * 128 + wave * 32 + (lane & 31);
   const bool qok = qloc < len;
   const int hl = lane >> 5;
@@ -414,9 +430,10 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = blockIdx.y;
+  int tile_id, h;
+  xcd_tile(tile_id, h);
   int seq0, len, kt;
-  locate(a.sg, blockIdx.x, 128 * KW, seq0, len, kt);
+  locate(a.sg, tile_id, 128 * KW, seq0, len, kt);
   int kloc[KW];
   bool kok[KW];
 #pragma unroll
@@ -586,9 +603,10 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = blockIdx.y;
+  int tile_id, h;
+  xcd_tile(tile_id, h);
   int seq0, len, qt;
-  locate(a.sg, blockIdx.x, 128 * QW, seq0, len, qt);
+  locate(a.sg, tile_id, 128 * QW, seq0, len, qt);
   const int hl = lane >> 5;
   int qloc[QW];
   bool qok[QW];

@@ -161,6 +161,17 @@ int vj_cast_bf16(long n, const float* in, void* out, void* stream);
  * data-gradient GEMM dX = dY W (nn.Linear backward) reads as its B operand. */
 int vj_transpose_bf16(int rows, int cols, const void* src, long ld_src, void* dst, long ld_dst, void* stream);
 
+/* JEPA multi-block 3-D masks on the device (src/masks/multiseq_multiblock3d.py:155-239): the host
+ * makes the reference's RNG draws (block size, (start, top, left) per block: boxes int32
+ * [B][npred][3]); vj_mask_count writes each sample's kept-token count, vj_mask_emit the ascending
+ * context / target id lists truncated to k_enc / k_pred (int64 [B][K]; mode 1 = full_complement,
+ * 2 = pred_full_complement: the complement of the other list). Replaces the per-sample
+ * torch.ones / slicing / argwhere / nonzero / default_collate of _MaskGenerator.__call__. */
+int vj_mask_count(int B, int duration, int height, int width, int npred, const int* boxes, int t, int h, int w,
+                  int max_ctx, int* counts, void* stream);
+int vj_mask_emit(int B, int duration, int height, int width, int npred, const int* boxes, int t, int h, int w,
+                 int max_ctx, int mode, int k_enc, int k_pred, long* enc, long* pred, void* stream);
+
 /* fp32-operand parity mode (vj_f32.hip): the encoder forward with f32 operands throughout, to show
  * the bf16 path's distance from the fp32 reference is operand rounding only. Not on the training
  * path. vj_gemm_f32: C = A B^T + bias (+ resid), epi as vj_gemm_bf16 (F32 = 1, F32_RESID = 2,

@@ -61,11 +61,15 @@ def test_main_matches_reference_trajectory(tmp_path, monkeypatch):
     losses = train.main(args)
     assert len(losses) == len(g["losses"]) == 6
     rep = []
+    from vjepa2_amd.masks import MaskSpec, materialize
+
     for i, (s, ref) in enumerate(zip(seen, g["samples"])):
-        (batch, menc, mpred), = s
+        entry, = s
+        assert all(isinstance(m, MaskSpec) for m in entry[1]), "main builds its masks on the GPU (data.gpu_masks)"
+        batch, menc, mpred = materialize(entry, "cuda")  # the same device build the step consumed
         assert abs(batch[0][0].double().sum().item() - float(ref["clip_sum"])) < 1e-3, f"clips of step {i}"
         for a, b in zip(menc + mpred, ref["enc"] + ref["pred"]):
-            assert torch.equal(a, b), f"masks of step {i} differ from the reference's"
+            assert torch.equal(a.cpu(), b), f"masks of step {i} differ from the reference's"
     for i, (l, r) in enumerate(zip(losses, g["losses"])):
         e = abs(l - r) / abs(r)
         rep.append(f"step {i}: loss {l:.6f} reference {r:.6f} rel {e:.2e}")

@@ -1057,3 +1057,131 @@ extern "C" int vj_quant_rows_fp8(int M, int K, const void* x, int x_bf16, long l
   VJ_LAUNCH_CHECK("vj_quant_rows_fp8");
   return VJ_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// JEPA multi-block 3-D masks on the device (src/masks/multiseq_multiblock3d.py:155-239). The host
+// draws the block size and positions with the reference's RNG calls (they define the stream) and
+// rejects empty contexts as it draws; the device builds every sample's context / target id lists:
+// token (f, r, c) is KEPT unless it lies in one of the npred blocks [start, start+t) x [top, top+h)
+// x [left, left+w) or f >= max_ctx (the context frame limit, :165-169). Lists are ascending (the
+// torch.nonzero / argwhere order), truncated to the batch minimum (:210-215) and written as the
+// int64 [B, K] tensors the step consumes.
+namespace {
+
+constexpr int MASK_THREADS = 256;
+
+__device__ __forceinline__ bool mask_kept(int tok, int HW, int W, int npred, const int* __restrict__ box, int t, int h,
+                                          int w, int max_ctx) {
+  const int f = tok / HW, rem = tok - f * HW, r = rem / W, c = rem - r * W;
+  if (f >= max_ctx) return false;
+  for (int j = 0; j < npred; ++j) {
+    const int s = box[3 * j], tp = box[3 * j + 1], lf = box[3 * j + 2];
+    if (f >= s && f < s + t && r >= tp && r < tp + h && c >= lf && c < lf + w) return false;
+  }
+  return true;
+}
+
+// exclusive block scan of one int per thread (MASK_THREADS threads)
+__device__ __forceinline__ int mask_scan(int v, int* sh, int& total) {
+  const int tid = threadIdx.x;
+  sh[tid] = v;
+  __syncthreads();
+  for (int o = 1; o < MASK_THREADS; o <<= 1) {
+    const int x = tid >= o ? sh[tid - o] : 0;
+    __syncthreads();
+    sh[tid] += x;
+    __syncthreads();
+  }
+  total = sh[MASK_THREADS - 1];
+  const int excl = sh[tid] - v;
+  __syncthreads();
+  return excl;
+}
+
+// per-sample number of kept tokens
+__global__ __launch_bounds__(MASK_THREADS) void k_mask_count(int N, int HW, int W, int npred, const int* __restrict__ boxes,
+                                                              int t, int h, int w, int max_ctx, int* __restrict__ counts) {
+  __shared__ int sh[MASK_THREADS];
+  const int b = blockIdx.x;
+  const int* box = boxes + (long)b * npred * 3;
+  int n = 0;
+  for (int tok = threadIdx.x; tok < N; tok += MASK_THREADS) n += mask_kept(tok, HW, W, npred, box, t, h, w, max_ctx);
+  int total;
+  mask_scan(n, sh, total);
+  if (threadIdx.x == 0) counts[b] = total;
+}
+
+// mode 0: enc = first k_enc kept ids, pred = first k_pred masked ids; 1 (full_complement): pred =
+// complement of enc; 2 (pred_full_complement): enc = complement of pred. Each thread owns a
+// contiguous token chunk, so the block scan of chunk counts yields ascending output order.
+__global__ __launch_bounds__(MASK_THREADS) void k_mask_emit(int N, int HW, int W, int npred, const int* __restrict__ boxes,
+                                                             int t, int h, int w, int max_ctx, int mode, int k_enc,
+                                                             int k_pred, long* __restrict__ enc, long* __restrict__ pred) {
+  __shared__ int sh[MASK_THREADS];
+  const int b = blockIdx.x;
+  const int* box = boxes + (long)b * npred * 3;
+  const int per = (N + MASK_THREADS - 1) / MASK_THREADS;
+  const int t0 = threadIdx.x * per, t1 = min(N, t0 + per);
+  int nk = 0;
+  for (int tok = t0; tok < t1; ++tok) nk += mask_kept(tok, HW, W, npred, box, t, h, w, max_ctx);
+  int tot_k;
+  const int rk = mask_scan(nk, sh, tot_k);  // kept ids before this chunk
+  const int rm = t0 - rk;                   // masked ids before this chunk
+  // ranks among the emitted lists: enc keeps kept ids with rank < k_enc (mode 0 / 1) or everything
+  // outside pred[:k_pred] (mode 2); pred symmetric
+  int ne = 0, np = 0;
+  {
+    int ik = rk, im = rm;
+    for (int tok = t0; tok < t1; ++tok) {
+      const bool kept = mask_kept(tok, HW, W, npred, box, t, h, w, max_ctx);
+      const bool in_enc = mode == 2 ? !(!kept && im < k_pred) : (kept && ik < k_enc);
+      const bool in_pred = mode == 1 ? !(kept && ik < k_enc) : (!kept && im < k_pred);
+      ne += in_enc;
+      np += in_pred;
+      ik += kept;
+      im += !kept;
+    }
+  }
+  int tot_e, tot_p;
+  int oe = mask_scan(ne, sh, tot_e);
+  int op = mask_scan(np, sh, tot_p);
+  long* erow = enc + (long)b * (mode == 2 ? N - k_pred : k_enc);
+  long* prow = pred + (long)b * (mode == 1 ? N - k_enc : k_pred);
+  int ik = rk, im = rm;
+  for (int tok = t0; tok < t1; ++tok) {
+    const bool kept = mask_kept(tok, HW, W, npred, box, t, h, w, max_ctx);
+    const bool in_enc = mode == 2 ? !(!kept && im < k_pred) : (kept && ik < k_enc);
+    const bool in_pred = mode == 1 ? !(kept && ik < k_enc) : (!kept && im < k_pred);
+    if (in_enc) erow[oe++] = tok;
+    if (in_pred) prow[op++] = tok;
+    ik += kept;
+    im += !kept;
+  }
+}
+
+}  // namespace
+
+extern "C" int vj_mask_count(int B, int duration, int height, int width, int npred, const int* boxes, int t, int h,
+                             int w, int max_ctx, int* counts, void* stream) {
+  if (B == 0) return VJ_OK;
+  VJ_CHECK_ARG(B > 0 && duration > 0 && height > 0 && width > 0 && npred >= 1 && boxes && counts,
+               "vj_mask_count: bad arguments");
+  const int N = duration * height * width;
+  hipLaunchKernelGGL(k_mask_count, dim3(B), dim3(MASK_THREADS), 0, (hipStream_t)stream, N, height * width, width, npred,
+                     boxes, t, h, w, max_ctx, counts);
+  VJ_LAUNCH_CHECK("vj_mask_count");
+  return VJ_OK;
+}
+
+extern "C" int vj_mask_emit(int B, int duration, int height, int width, int npred, const int* boxes, int t, int h,
+                            int w, int max_ctx, int mode, int k_enc, int k_pred, long* enc, long* pred, void* stream) {
+  if (B == 0) return VJ_OK;
+  const int N = duration * height * width;
+  VJ_CHECK_ARG(B > 0 && N > 0 && npred >= 1 && boxes && enc && pred && mode >= 0 && mode <= 2,
+               "vj_mask_emit: bad arguments");
+  VJ_CHECK_ARG(k_enc >= 0 && k_enc <= N && k_pred >= 0 && k_pred <= N, "vj_mask_emit: bad lengths");
+  hipLaunchKernelGGL(k_mask_emit, dim3(B), dim3(MASK_THREADS), 0, (hipStream_t)stream, N, height * width, width, npred,
+                     boxes, t, h, w, max_ctx, mode, k_enc, k_pred, enc, pred);
+  VJ_LAUNCH_CHECK("vj_mask_emit");
+  return VJ_OK;
+}

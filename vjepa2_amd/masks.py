@@ -9,13 +9,18 @@ block). Masks are sorted ascending int64 token ids, truncated to the batch minim
 import math
 from multiprocessing import Value
 
+import numpy as np
 import torch
 
 
 class MaskCollator:
     """multiseq_multiblock3d.py:16-76: one generator per (frames-per-clip, mask config)."""
 
-    def __init__(self, cfgs_mask, dataset_fpcs, crop_size=(224, 224), patch_size=(16, 16), tubelet_size=2):
+    def __init__(self, cfgs_mask, dataset_fpcs, crop_size=(224, 224), patch_size=(16, 16), tubelet_size=2,
+                 device_masks=False):
+        # device_masks: the collate (a data-loader worker) only makes the reference's RNG draws and
+        # returns MaskSpec objects; materialize() builds the masks on the GPU in the training process
+        self.device_masks = device_masks
         self.mask_generators = {}
         for fpc in dataset_fpcs:
             self.mask_generators[fpc] = [
@@ -42,6 +47,9 @@ class MaskCollator:
             if not samples:
                 continue
             collated = torch.utils.data.default_collate(samples)
+            if self.device_masks:
+                out.append((collated, [gen.draw(len(samples)) for gen in self.mask_generators[fpc]], None))
+                continue
             enc, pred = [], []
             for gen in self.mask_generators[fpc]:
                 e, p = gen(len(samples))
@@ -104,6 +112,32 @@ class _MaskGenerator:
             grid *= blk
         return grid.flatten()
 
+    def draw(self, batch_size):
+        """The reference's RNG draws for one collate, nothing else (host, in the data-loader worker):
+        the block size from the iteration-seeded generator, npred (top, left, start) positions per
+        sample from the global RNG in the reference's call order, redrawn while a sample's context
+        would be empty (:191-208; decided on a boolean grid). Returns a MaskSpec."""
+        g = torch.Generator()
+        g.manual_seed(self.step())
+        t, h, w = self._block_size(g)
+        boxes = np.empty((batch_size, self.npred, 3), dtype=np.int32)
+        grid = np.empty((self.duration, self.height, self.width), dtype=bool)
+        for b in range(batch_size):
+            while True:
+                grid.fill(True)
+                grid[self.max_context_duration:] = False
+                for j in range(self.npred):
+                    top = int(torch.randint(0, self.height - h + 1, (1,)))
+                    left = int(torch.randint(0, self.width - w + 1, (1,)))
+                    start = int(torch.randint(0, self.duration - t + 1, (1,)))
+                    boxes[b, j] = (start, top, left)
+                    grid[start:start + t, top:top + h, left:left + w] = False
+                if grid.any():
+                    break
+        return MaskSpec((self.duration, self.height, self.width), (t, h, w), self.max_context_duration, boxes,
+                        self.max_keep, 1 if self.full_complement else (2 if self.pred_full_complement else 0),
+                        self.inv_block)
+
     def __call__(self, batch_size):
         g = torch.Generator()
         g.manual_seed(self.step())
@@ -138,3 +172,52 @@ def _complement(ids, total):
     keep = torch.ones(total, dtype=torch.bool)
     keep[ids] = False
     return torch.nonzero(keep).reshape(-1).to(ids.dtype)
+
+
+class MaskSpec:
+    """One mask config's draws for one collate (picklable, a few hundred bytes): grid (duration,
+    height, width), block size (t, h, w), context frame limit, block positions int32 [B, npred, 3]
+    as (start, top, left), max_keep, complement mode (0, 1 = full_complement, 2 =
+    pred_full_complement), inv_block."""
+
+    __slots__ = ("grid", "size", "max_ctx", "boxes", "max_keep", "mode", "inv_block")
+
+    def __init__(self, grid, size, max_ctx, boxes, max_keep, mode, inv_block):
+        self.grid, self.size, self.max_ctx, self.boxes = tuple(grid), tuple(size), int(max_ctx), boxes
+        self.max_keep, self.mode, self.inv_block = max_keep, int(mode), bool(inv_block)
+
+    def build(self, device):
+        """(masks_enc, masks_pred) int64 [B, K] on `device` (vj_mask_count / vj_mask_emit), equal to
+        what _MaskGenerator.__call__ returns for the same draws. One host sync: the batch-minimum
+        lengths size the outputs."""
+        from . import ops
+
+        duration, height, width = self.grid
+        t, h, w = self.size
+        B, npred = self.boxes.shape[0], self.boxes.shape[1]
+        N = duration * height * width
+        boxes = torch.from_numpy(self.boxes).to(device)
+        counts = torch.empty(B, dtype=torch.int32, device=device)
+        ops.mask_count(B, duration, height, width, npred, boxes, t, h, w, self.max_ctx, counts)
+        kept = counts.cpu()
+        k_enc, k_pred = int(kept.min()), int(N - kept.max())
+        if self.max_keep is not None:
+            k_enc = min(k_enc, int(self.max_keep))
+        le = N - k_pred if self.mode == 2 else k_enc
+        lp = N - k_enc if self.mode == 1 else k_pred
+        enc = torch.empty(B, le, dtype=torch.int64, device=device)
+        pred = torch.empty(B, lp, dtype=torch.int64, device=device)
+        ops.mask_emit(B, duration, height, width, npred, boxes, t, h, w, self.max_ctx, self.mode, k_enc, k_pred, enc,
+                      pred)
+        return (pred, enc) if self.inv_block else (enc, pred)
+
+
+def materialize(entry, device):
+    """One collated (fpc-group) entry -> (clips, masks_enc list, masks_pred list) with the masks on
+    `device`: host masks are copied, MaskSpecs are built there."""
+    collated, enc, pred = entry
+    if pred is None:  # device_masks collate: enc holds one MaskSpec per mask config
+        built = [spec.build(device) for spec in enc]
+        return collated, [e for e, _ in built], [p for _, p in built]
+    return (collated, [m.to(device, non_blocking=True) for m in enc],
+            [m.to(device, non_blocking=True) for m in pred])

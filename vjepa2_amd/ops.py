@@ -517,3 +517,20 @@ def im2col_f32(clip, patch, tub, idx=None):
     out = torch.empty(B * K, C * tub * patch * patch, dtype=F32, device=clip.device)
     _call("vj_im2col_tubelet_f32", B * K, K, _p(idx), B, C, Tf, Hf, Wf, tub, patch, _p(clip), _p(out), _stream())
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# JEPA masks on the device (masks.MaskSpec.build)
+
+
+def mask_count(B, duration, height, width, npred, boxes, t, h, w, max_ctx, counts):
+    _dev(boxes, counts)
+    assert boxes.dtype == torch.int32 and boxes.is_contiguous() and boxes.shape == (B, npred, 3)
+    _call("vj_mask_count", B, duration, height, width, npred, _p(boxes), t, h, w, max_ctx, _p(counts), _stream())
+
+
+def mask_emit(B, duration, height, width, npred, boxes, t, h, w, max_ctx, mode, k_enc, k_pred, enc, pred):
+    _dev(boxes, enc, pred)
+    assert enc.dtype == torch.int64 and pred.dtype == torch.int64 and enc.is_contiguous() and pred.is_contiguous()
+    _call("vj_mask_emit", B, duration, height, width, npred, _p(boxes), t, h, w, max_ctx, mode, k_enc, k_pred,
+          _p(enc), _p(pred), _stream())

@@ -29,7 +29,7 @@ from . import predictor as vit_pred
 from . import vision_transformer as video_vit
 from .arena import FlatArena, FusedAdamW, fused_ema, readiness_order, wd_split
 from .distributed import GradReducer, init_distributed
-from .masks import MaskCollator
+from .masks import MaskCollator, materialize
 from .schedulers import CosineWDSchedule, WarmupCosineSchedule
 from .wrappers import MultiSeqWrapper, PredictorMultiSeqWrapper
 
@@ -351,8 +351,11 @@ def main(args, resume_preempt=False):
         use_pred_silu=cm.get("use_pred_silu", False), wide_silu=cm.get("wide_silu", True),
         use_activation_checkpointing=cm.get("use_activation_checkpointing", False))
     target_encoder = copy.deepcopy(encoder)
+    # masks built on the GPU from the collate's RNG draws (bit-exact with the host collate);
+    # data.gpu_masks: false keeps the reference's host-side masks
     mask_collator = MaskCollator(cfgs_mask=cfgs_mask, dataset_fpcs=dataset_fpcs, crop_size=crop_size,
-                                 patch_size=patch_size, tubelet_size=tubelet_size)
+                                 patch_size=patch_size, tubelet_size=tubelet_size,
+                                 device_masks=bool(cd.get("gpu_masks", True)))
     loader, sampler = init_data(batch_size=batch_size, collator=mask_collator, dataset_fpcs=dataset_fpcs,
                                 crop_size=crop_size, rank=rank, world_size=world_size,
                                 num_workers=cd.get("num_workers", 0))
@@ -389,9 +392,10 @@ def main(args, resume_preempt=False):
             except StopIteration:
                 loader_it = iter(loader)
                 sample = next(loader_it)
+            sample = [materialize(s, device) for s in sample]
             clips = [s[0][0][0].to(device, non_blocking=True) for s in sample]
-            menc = [[m.to(device, non_blocking=True) for m in s[1]] for s in sample]
-            mpred = [[m.to(device, non_blocking=True) for m in s[2]] for s in sample]
+            menc = [s[1] for s in sample]
+            mpred = [s[2] for s in sample]
             data_ms = (time.time() - t0) * 1000.0
 
             def step():

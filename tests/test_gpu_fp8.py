@@ -103,11 +103,15 @@ def test_fp8_gemm_matches_dequantized(M, N, K):
     assert ((y.cpu() - (exp + resid)).abs() <= bound + 2.0 ** -23 * (exp.abs() + resid.abs())).all()
     yb = ops.linear_fwd_fp8(a8, ea, w8, ew, bias.to(DEV), ops.EPI_BF16)
     assert (yb.cpu().float() - exp).abs().max().item() <= 2 ** -7 * exp.abs().max().item()
-    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-    _, act = ops.linear_fwd_fp8(a8, ea, w8, ew, bias.to(DEV), ops.EPI_GELU, out=pre)
+    pre = ops.linear_fwd_fp8(a8, ea, w8, ew, bias.to(DEV), ops.EPI_BF16)  # the bf16 pre-activation
+    dg = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    _, act = ops.linear_fwd_fp8(a8, ea, w8, ew, bias.to(DEV), ops.EPI_GELU, out=dg)
     torch.cuda.synchronize()
-    ga = torch.nn.functional.gelu(pre.cpu().float())
-    assert (act.cpu().float() - ga).abs().max().item() <= 2 ** -7 * ga.abs().max().item() + 1e-3
+    xp = pre.cpu().float().requires_grad_(True)
+    ga = torch.nn.functional.gelu(xp)
+    ga.sum().backward()
+    assert (act.cpu().float() - ga.detach()).abs().max().item() <= 2 ** -7 * ga.abs().max().item() + 1e-3
+    assert (dg.cpu().float() - xp.grad).abs().max().item() <= 2 ** -7 * 1.2 + 1e-3
 
 
 def test_fp8_qkv_rope_matches_dequantized():

@@ -103,27 +103,36 @@ def test_gemm_epilogues(M, N):
     resid = torch.randn(M, N, generator=g).to(DEV)
     y = ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid)
     _close(y, ref + resid, 2e-4, 1e-5, "EPI_F32_RESID")
-    pre, act = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
-    _close(pre, ref, 1e-3, 8e-3, "EPI_GELU pre")
-    _close(act, torch.nn.functional.gelu(pre.float()), 1e-3, 8e-3, "EPI_GELU act")
-    if M >= 1024:  # GELU of the bf16 pre-activation, rounded once (erf polynomial, |err| <= 1.5e-7)
-        exact = act == torch.nn.functional.gelu(pre.float()).bfloat16()
-        assert float(exact.float().mean()) > 0.995  # erf polynomial: 1-ulp ties at rounding boundaries
-    # GELU backward epilogue: out = (dY W) * gelu'(pre)
+    pre = ops.linear_fwd(X, W, b, ops.EPI_BF16)  # the same bf16 pre-activation the GELU epilogue rounds
+    dgelu, act = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
+    _, act2 = ops.linear_fwd(X, W, b, ops.EPI_GELU)  # no derivative requested (no-grad target path)
+    assert torch.equal(act, act2)
+    xp = pre.float().requires_grad_(True)
+    yp = torch.nn.functional.gelu(xp)
+    yp.backward(torch.ones_like(yp))
+    _close(act, yp.detach(), 1e-3, 8e-3, "EPI_GELU act")
+    _close(dgelu, xp.grad, 1e-3, 8e-3, "EPI_GELU saved derivative")
+    # GELU of the bf16 pre-activation, rounded once (erf polynomial, |err| <= 1.5e-7): 1-ulp ties only
+    assert float((act == yp.detach().bfloat16()).float().mean()) > 0.995
+    assert float((dgelu == xp.grad.bfloat16()).float().mean()) > 0.995
+    # GELU backward epilogue: out = (dY W) * saved derivative
     dY = torch.randn(M, N, generator=g).to(DEV).bfloat16()
     W2 = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
     pre2 = torch.randn(M, K, generator=g).to(DEV).bfloat16()
     x = pre2.float().requires_grad_(True)
     torch.nn.functional.gelu(x).backward(dY.float() @ W2.float())
-    got = ops.linear_dgrad(dY, W2, gelu_pre=pre2)
-    _close(got, x.grad, 2e-3, 1e-2, "EPI_GELU_BWD")
+    xd = pre2.float().requires_grad_(True)
+    torch.nn.functional.gelu(xd).sum().backward()
+    dg2 = xd.grad.bfloat16()  # what the forward epilogue saves
+    got = ops.linear_dgrad(dY, W2, gelu_grad=dg2)
+    _close(got, x.grad, 2e-3, 1.5e-2, "EPI_GELU_BWD")
     # the same with B K-major (direct-store epilogue) and the plain f32 epilogue
     W2t = W2.t().contiguous()  # [K, N]: B(n=k_out, k=n_in) K-major
     got2 = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
-    ops.gemm(M, K, N, dY, N, True, W2t, N, True, ops.EPI_GELU_BWD, out=got2, ldc=K, aux=pre2, ldaux=K)
-    _close(got2, x.grad, 2e-3, 1e-2, "EPI_GELU_BWD (B K-major)")
-    got3 = ops.linear_dgrad(dY, W2, gelu_pre=pre2, wt=ops.transpose_bf16(W2))
-    _close(got3, x.grad, 2e-3, 1e-2, "EPI_GELU_BWD (linear_dgrad on W^T)")
+    ops.gemm(M, K, N, dY, N, True, W2t, N, True, ops.EPI_GELU_BWD, out=got2, ldc=K, aux=dg2, ldaux=K)
+    _close(got2, x.grad, 2e-3, 1.5e-2, "EPI_GELU_BWD (B K-major)")
+    got3 = ops.linear_dgrad(dY, W2, gelu_grad=dg2, wt=ops.transpose_bf16(W2))
+    _close(got3, x.grad, 2e-3, 1.5e-2, "EPI_GELU_BWD (linear_dgrad on W^T)")
     f32 = torch.empty(M, K, device=DEV)
     ops.gemm(M, K, N, dY, N, True, W2t, N, True, ops.EPI_F32, out=f32, ldc=K)
     _close(f32, dY.float() @ W2.float(), 2e-4 * math.sqrt(N), 1e-5, "EPI_F32 (B K-major)")

@@ -39,6 +39,7 @@ GEMMS = [
     ("fc1  ctx", 11712, 4096, 1024, 1, 1, 3, 1),
     ("fc2  ctx", 11712, 1024, 4096, 1, 1, 2, 1),
     ("fc1  tgt", 49152, 4096, 1024, 1, 1, 3, 1),
+    ("fc1  ctx save", 11712, 4096, 1024, 1, 1, 7, 1),  # 7: GELU with the derivative saved (training path)
     ("qkv  tgt", 49152, 3072, 1024, 1, 1, 0, 1),
     ("proj tgt", 49152, 1024, 1024, 1, 1, 2, 1),
     ("proj tgt f32", 49152, 1024, 1024, 1, 1, 1, 1),
@@ -59,6 +60,7 @@ GEMMS = [
     ("pred dgrad fc1", 71232, 384, 1536, 1, 0, 0, 1),
     ("pred wgrad fc1", 1536, 384, 71232, 0, 0, 2, 14),
     ("pred fc1", 71232, 1536, 384, 1, 1, 3, 1),
+    ("pred fc1 save", 71232, 1536, 384, 1, 1, 7, 1),
     ("pred fc2", 71232, 384, 1536, 1, 1, 2, 1),
 ]
 
@@ -77,6 +79,8 @@ ATTN = [("attn fwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], False),
 
 def gemm_case(lib, case, dev, stream):
     name, M, N, K, akm, bkm, epi, sk = case
+    save_d = epi == 7
+    epi = 3 if save_d else epi
     g = torch.Generator(device="cpu").manual_seed(0)
     A = ((torch.rand(M, K, generator=g) * 2 - 1) if akm else (torch.rand(K, M, generator=g) * 2 - 1)).to(dev).bfloat16()
     B = ((torch.rand(N, K, generator=g) * 2 - 1) if bkm else (torch.rand(K, N, generator=g) * 2 - 1)).to(dev).bfloat16()
@@ -94,7 +98,8 @@ def gemm_case(lib, case, dev, stream):
 
     def run():
         rc = lib.vj_gemm_bf16_splitk(M, N, K, p(A), lda, akm, p(B), ldb, bkm, epi, p(bias), p(aux), N if aux is not None else 0,
-                                     p(C) if epi != 3 else None, N if epi != 3 else 0, p(C2), N if C2 is not None else 0,
+                                     p(C) if epi != 3 or save_d else None, N if epi != 3 or save_d else 0, p(C2),
+                                     N if C2 is not None else 0,
                                      sk, p(ws), ws.numel(), stream)
         assert rc == 0, rc
     return run, 2.0 * M * N * K

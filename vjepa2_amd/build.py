@@ -35,23 +35,6 @@ def _torch_libdir():
         return None
 
 
-GEN = os.path.join(HERE, "build", "gen")
-
-
-def _gen_headers():
-    """Generated device headers (GELU tables), rebuilt when their generator changes."""
-    os.makedirs(GEN, exist_ok=True)
-    hdr = os.path.join(GEN, "vj_gelu_tables.h")
-    gen_src = os.path.join(HERE, "gelu_tables.py")
-    if not os.path.exists(hdr) or os.path.getmtime(gen_src) > os.path.getmtime(hdr):
-        sys.path.insert(0, os.path.dirname(HERE))
-        from vjepa2_amd import gelu_tables
-
-        gelu_tables.write_header(hdr + ".tmp")
-        os.replace(hdr + ".tmp", hdr)
-    return [hdr]
-
-
 def _needs_build(obj, src, extra=()):
     deps = [src, os.path.join(CSRC, "vj_common.h"), *extra]
     return not os.path.exists(obj) or any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
@@ -63,15 +46,14 @@ def build(verbose=True, force=False, variant=None, defines=()):
     A/B timing of kernel variants inside one process (tools/bench_kernels.py)."""
     objdir = os.path.join(HERE, "build", variant) if variant else os.path.join(HERE, "build")
     lib = os.path.join(HERE, f"libvjepa_hip_{variant}.so") if variant else LIB
-    gen = _gen_headers()
-    flags = CFLAGS + [f"-I{GEN}"] + [f"-D{d}" for d in defines]
+    flags = CFLAGS + [f"-D{d}" for d in defines]
     os.makedirs(objdir, exist_ok=True)
     jobs = []
     csrc = os.environ.get("VJ_CSRC", CSRC) if variant else CSRC  # variant may build another source tree
     for s in SOURCES:
         src = os.path.join(csrc, s)
         obj = os.path.join(objdir, s.replace(".hip", ".o"))
-        if force or variant or _needs_build(obj, src, gen):
+        if force or variant or _needs_build(obj, src):
             jobs.append([HIPCC, *flags, *SRC_FLAGS.get(s, []), "-c", src, "-o", obj])
 
     def run(cmd):

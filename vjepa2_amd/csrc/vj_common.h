@@ -113,17 +113,13 @@ __device__ __forceinline__ uint32_t f8pack4(float a, float b, float c, float d) 
   return (uint32_t)w;
 }
 
-__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
-}
-
 static inline int vj_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
-// erf with |abs err| <= 1.5e-7 (Abramowitz-Stegun 7.1.26): far below the bf16 rounding of the output.
-__device__ __forceinline__ float erf_fast(float z) {
+// nn.GELU() (exact erf form, vision_transformer.py:100) and its derivative in one pass (the erf
+// and Gaussian terms are shared). erf by Abramowitz-Stegun 7.1.26, |abs err| <= 1.5e-7: far below
+// the bf16 rounding of the outputs.
+__device__ __forceinline__ void gelu_fwd_grad(float x, float& y, float& dy) {
+  const float z = x * 0.70710678118654752f;
   const float a = fabsf(z);
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
   float p = fmaf(1.061405429f, t, -1.453152027f);
@@ -131,13 +127,10 @@ __device__ __forceinline__ float erf_fast(float z) {
   p = fmaf(p, t, -0.284496736f);
   p = fmaf(p, t, 0.254829592f);
   p *= t;
-  const float r = 1.f - p * __expf(-a * a);
-  return copysignf(r, z);
-}
-// nn.GELU() (exact erf form, vision_transformer.py:100) and its derivative
-__device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad_fast(float x) {
-  return 0.5f * (1.f + erf_fast(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+  const float e = __expf(-a * a);  // exp(-x^2 / 2)
+  const float cdf = 0.5f * (1.f + copysignf(1.f - p * e, z));
+  y = x * cdf;
+  dy = fmaf(x * 0.39894228040143268f, e, cdf);
 }
 
 // 3-axis RoPE applied to the q and k columns of a fused QKV projection (modules.py:26-50, 343-365),

@@ -35,7 +35,7 @@ struct GemmArgs {
   void* C2;
   long ldc2;
   const float* bias;
-  const void* aux;  // EPI_GELU_BWD: bf16 pre-activation; EPI_F32_RESID: f32 residual input
+  const void* aux;  // EPI_GELU_BWD: bf16 GELU derivative (saved by EPI_GELU); EPI_F32_RESID: f32 residual
   long ldaux;
   int kslice;  // split-K: K range of blockIdx.z is [z*kslice, min(K, (z+1)*kslice))
   float* ws;   // EPI_PARTIAL: f32 partial tiles [splitk][M][N]
@@ -179,12 +179,13 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
           const float res = ((const float*)g.aux)[(long)m * g.ldaux + n];
           ((float*)g.C)[(long)m * g.ldc + n] = res + v;
         } else if constexpr (EPI == EPI_GELU) {
-          const bf16_t pre = f2bf(v);
-          if (g.C) ((bf16_t*)g.C)[(long)m * g.ldc + n] = pre;
-          ((bf16_t*)g.C2)[(long)m * g.ldc2 + n] = f2bf(gelu_f(bf2f(pre)));
+          float y, dy;
+          gelu_fwd_grad(bf2f(f2bf(v)), y, dy);  // on the bf16 pre-activation
+          if (g.C) ((bf16_t*)g.C)[(long)m * g.ldc + n] = f2bf(dy);  // saved for EPI_GELU_BWD
+          ((bf16_t*)g.C2)[(long)m * g.ldc2 + n] = f2bf(y);
         } else if constexpr (EPI == EPI_GELU_BWD) {
-          const float pre = bf2f(((const bf16_t*)g.aux)[(long)m * g.ldaux + n]);
-          ((bf16_t*)g.C)[(long)m * g.ldc + n] = f2bf(acc[i][j][r] * gelu_grad_f(pre));
+          const float dg = bf2f(((const bf16_t*)g.aux)[(long)m * g.ldaux + n]);  // saved GELU derivative
+          ((bf16_t*)g.C)[(long)m * g.ldc + n] = f2bf(acc[i][j][r] * dg);
         }
       }
     }

@@ -20,17 +20,7 @@
 #include <stdlib.h>
 #include <type_traits>
 #include "vj_common.h"
-#include "vj_gelu_tables.h"  // generated by build.py from vjepa2_amd/gelu_tables.py
 
-// GELU in the epilogues: table lookup (exact reference fp32 formula on bf16 inputs) or the erf
-// polynomial. Measured: the lookup's index/range logic costs as much VALU as the polynomial for the
-// forward, so the forward keeps the polynomial; the derivative (erf + exp) uses the table.
-#ifndef VJ_GELU_TABLE_FWD
-#define VJ_GELU_TABLE_FWD 0
-#endif
-#ifndef VJ_GELU_TABLE_BWD
-#define VJ_GELU_TABLE_BWD 1
-#endif
 // Waves that issue the LDS-DMA of a K stage: 8 (all) or 4 (waves 0-3, so their SIMD partners 4-7
 // keep the matrix pipe busy while the DMA issues)
 #ifndef VJ_GEMM_DMA_WAVES
@@ -140,35 +130,16 @@ __device__ __forceinline__ bf16x8 frag(const LDS_AS char* lds, int rb, int s, in
   }
 }
 
-// Table GELU (vjepa2_amd/gelu_tables.py): exactly the reference's fp32 formula on a bf16 input.
-// b = bf16 bits of x. In-range exponents read the LDS table; the rest use the closed forms.
-constexpr int GELU_FWD_WORDS = VJ_GELU_N / 2;  // u16 table packed in u32
-constexpr int GELU_BWD_WORDS = VJ_GELU_N;
-static_assert(GELU_BWD_WORDS * 4 <= TAB_BYTES, "GELU table must fit the LDS table area");
-__device__ __forceinline__ uint32_t gelu_slot(uint32_t b, bool& in, bool& tiny) {
-  const uint32_t e = (b >> 7) & 0xff, rel = e - (uint32_t)VJ_GELU_ELO;
-  in = rel < (uint32_t)VJ_GELU_NEXP;
-  tiny = e < (uint32_t)VJ_GELU_ELO;
-  return in ? (b >> 15) * (VJ_GELU_NEXP * 128) + rel * 128 + (b & 127) : 0u;
-}
-__device__ __forceinline__ uint32_t gelu_tab_bf16(uint32_t b, const LDS_AS unsigned short* tab) {
-  bool in, tiny;
-  const uint32_t t = tab[gelu_slot(b, in, tiny)];
-  const uint32_t half = f2bf(bf2f(b) * 0.5f);
-  return in ? t : (tiny ? half : ((b & 0x8000) ? 0x8000u : b));
-}
-__device__ __forceinline__ float gelu_grad_tab(uint32_t b, const LDS_AS float* tab) {
-  bool in, tiny;
-  const float t = tab[gelu_slot(b, in, tiny)];
-  return in ? t : (tiny ? fmaf(0.7978845608f, bf2f(b), 0.5f) : ((b & 0x8000) ? 0.f : 1.f));
-}
-__device__ __forceinline__ uint32_t gelu_sel(uint32_t b, const LDS_AS unsigned short* tab) {
-  if constexpr (VJ_GELU_TABLE_FWD) return gelu_tab_bf16(b, tab);
-  else return pack_bf2(gelu_fast(bf2f(b)), 0.f) & 0xffff;
-}
-__device__ __forceinline__ float gelu_grad_sel(uint32_t b, const LDS_AS float* tab) {
-  if constexpr (VJ_GELU_TABLE_BWD) return gelu_grad_tab(b, tab);
-  else return gelu_grad_fast(bf2f(b));
+// GELU (nn.GELU(), vision_transformer.py:100) in the epilogues: the forward evaluates it on the bf16
+// pre-activation (the reference's autocast order) and, when the caller saves for the backward, the
+// derivative gelu'(pre) in the same pass (its erf and Gaussian terms are already computed); the
+// backward epilogue then multiplies by the saved derivative (one VALU op per element).
+__device__ __forceinline__ uint32_t gelu_pair(uint32_t pk, uint32_t* dpk) {
+  float y0, d0, y1, d1;
+  gelu_fwd_grad(__builtin_bit_cast(float, pk << 16), y0, d0);
+  gelu_fwd_grad(__builtin_bit_cast(float, pk & 0xffff0000u), y1, d1);
+  if (dpk) *dpk = pack_bf2(d0, d1);
+  return pack_bf2(y0, y1);
 }
 
 struct Tile {
@@ -268,20 +239,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
     load_k(rsrc_a(T), rsrc_b(T), T, t, slot, lane);
   };
 
-  // per-kernel tables: global loads issued before the first DMA (so their waits do not queue behind
-  // it), written to the table area after it; the first barrier of the tile loop publishes them
-  constexpr int GW = (EPI == EPI_GELU && VJ_GELU_TABLE_FWD) ? GELU_FWD_WORDS
-                     : ((EPI == EPI_GELU_BWD && VJ_GELU_TABLE_BWD) ? GELU_BWD_WORDS : 0);
-  constexpr int GWR = (GW + 511) / 512;
-  [[maybe_unused]] uint32_t gpf[GWR > 0 ? GWR : 1];
-  if constexpr (GW > 0) {
-#pragma unroll
-    for (int i = 0; i < GWR; ++i) {
-      const int w = threadIdx.x + 512 * i;
-      if constexpr (EPI == EPI_GELU) gpf[i] = w < GW ? vj_gelu_fwd_tab[w] : 0u;
-      else gpf[i] = w < GW ? __builtin_bit_cast(uint32_t, vj_gelu_bwd_tab[w]) : 0u;
-    }
-  }
+  // per-kernel tables (RoPE): global loads issued before the first DMA (so their waits do not queue
+  // behind it), written to the table area after it; the first barrier of the tile loop publishes them
   constexpr int RTR = EPI == EPI_ROPE ? (ROPE_TAB_MAX + 511) / 512 : 0;
   [[maybe_unused]] f32x2 rpf[RTR > 0 ? RTR : 1];
   [[maybe_unused]] const int ntab = EPI == EPI_ROPE ? g.rope.npos * g.rope.half : 0;  // <= ROPE_TAB_MAX (host)
@@ -295,22 +254,12 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
   // tile-row positions (frame | row << 10 | col << 20) and the interleaved cos/sin table (RoPE)
   [[maybe_unused]] LDS_AS int* rpos = (LDS_AS int*)tab;
   [[maybe_unused]] LDS_AS f32x2* rtab = (LDS_AS f32x2*)(tab + BM * 4);
-  [[maybe_unused]] const LDS_AS unsigned short* gtf = (const LDS_AS unsigned short*)tab;
-  [[maybe_unused]] const LDS_AS float* gtb = (const LDS_AS float*)tab;
 
   int wg = run0 + jb;
   Tile cur = make_tile(wg);
   int par = 0;  // LDS slot of K-tile t of the current tile: (t + par) & 1
   load_tile(cur, 0, 0, lane);
   if (cur.nk > 1) load_tile(cur, 1, 1, lane);
-  if constexpr (GW > 0) {
-    LDS_AS uint32_t* dst = (LDS_AS uint32_t*)tab;
-#pragma unroll
-    for (int i = 0; i < GWR; ++i) {
-      const int w = threadIdx.x + 512 * i;
-      if (w < GW) dst[w] = gpf[i];
-    }
-  }
   if constexpr (EPI == EPI_ROPE) {
 #pragma unroll
     for (int i = 0; i < RTR; ++i) {
@@ -602,14 +551,15 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
               dst[r][0] = x.x; dst[r][1] = x.y;
             }
           } else {
-            auto bits = [](uint32_t u) { return __builtin_bit_cast(float, u); };  // raw bf16 bits
-            if constexpr (NTN == 4) {
+            auto lo = [](uint32_t u) { return __builtin_bit_cast(float, u << 16); };  // bf16 -> f32, exact
+            auto hi = [](uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); };
+            if constexpr (NTN == 4) {  // saved GELU derivative
               const uint2 x = *(const uint2*)((const bf16_t*)g.aux + off);
-              dst[r][0] = bits(x.x & 0xffff); dst[r][1] = bits(x.x >> 16);
-              dst[r][2] = bits(x.y & 0xffff); dst[r][3] = bits(x.y >> 16);
+              dst[r][0] = lo(x.x); dst[r][1] = hi(x.x);
+              dst[r][2] = lo(x.y); dst[r][3] = hi(x.y);
             } else {
               const uint32_t x = *(const uint32_t*)((const bf16_t*)g.aux + off);
-              dst[r][0] = bits(x & 0xffff); dst[r][1] = bits(x >> 16);
+              dst[r][0] = lo(x); dst[r][1] = hi(x);
             }
           }
         }
@@ -640,6 +590,9 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
         }
       };
       if constexpr (AUX) fetch(0, aux[0]);
+      // GELU: the derivative pass is compiled separately, for callers that save it (g.C)
+      auto rows = [&](auto save_c) {
+      constexpr bool SAVE_D = decltype(save_c)::value;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         if constexpr (AUX) {
@@ -722,20 +675,22 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
 #pragma unroll
             for (int q2 = 0; q2 < 2; ++q2) {
               if constexpr (EPI == EPI_GELU_BWD)
-                pk[r][q2] = pack_bf2(v[2 * q2] * gelu_grad_sel(__builtin_bit_cast(uint32_t, aux[i & 1][r][2 * q2]), gtb),
-                                     v[2 * q2 + 1] * gelu_grad_sel(__builtin_bit_cast(uint32_t, aux[i & 1][r][2 * q2 + 1]), gtb));
+                pk[r][q2] = pack_bf2(v[2 * q2] * aux[i & 1][r][2 * q2], v[2 * q2 + 1] * aux[i & 1][r][2 * q2 + 1]);
               else
                 pk[r][q2] = pack_bf2(v[2 * q2], v[2 * q2 + 1]);
-              if constexpr (EPI == EPI_GELU)
-                ga[r][q2] = gelu_sel(pk[r][q2] & 0xffff, gtf) | (gelu_sel(pk[r][q2] >> 16, gtf) << 16);
+              if constexpr (EPI == EPI_GELU)  // pk: the bf16 pre-activation -> GELU, derivative (if saved)
+                ga[r][q2] = gelu_pair(pk[r][q2], SAVE_D ? &pk[r][q2] : nullptr);
             }
           }
         }
         if constexpr (!F32OUT) {
-          if (EPI != EPI_GELU || g.C) store_wide((bf16_t*)g.C, g.ldc, i, pk);
+          if (EPI != EPI_GELU || SAVE_D) store_wide((bf16_t*)g.C, g.ldc, i, pk);
           if constexpr (EPI == EPI_GELU) store_wide((bf16_t*)g.C2, g.ldc2, i, ga);
         }
       }
+      };
+      if (EPI == EPI_GELU && g.C) rows(std::true_type{});
+      else rows(std::false_type{});
     } else {
       const int lane = lane_e;
       // ---- staged epilogue: passes of MTP m-tiles (16*MTP rows) per wave through a padded image in
@@ -828,16 +783,16 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
             const float4 rr = rres[it];
             *(float4*)((float*)g.C + (long)m * g.ldc + n) = make_float4(rr.x + v[0], rr.y + v[1], rr.z + v[2], rr.w + v[3]);
           } else if constexpr (EPI == EPI_GELU) {
-            const uint32_t p0 = pack_bf2(v[0], v[1]), p1 = pack_bf2(v[2], v[3]);
-            if (g.C) *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(p0, p1);
-            *(uint2*)((bf16_t*)g.C2 + (long)m * g.ldc2 + n) =
-                make_uint2(gelu_sel(p0 & 0xffff, gtf) | (gelu_sel(p0 >> 16, gtf) << 16),
-                           gelu_sel(p1 & 0xffff, gtf) | (gelu_sel(p1 >> 16, gtf) << 16));
+            uint32_t d0, d1;
+            const uint32_t a0 = gelu_pair(pack_bf2(v[0], v[1]), &d0), a1 = gelu_pair(pack_bf2(v[2], v[3]), &d1);
+            if (g.C) *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(d0, d1);
+            *(uint2*)((bf16_t*)g.C2 + (long)m * g.ldc2 + n) = make_uint2(a0, a1);
           } else {  // EPI_GELU_BWD
-            const uint2 pu = rpre[it];
+            const uint2 pu = rpre[it];  // saved GELU derivative (bf16)
+            auto lo = [](uint32_t u) { return __builtin_bit_cast(float, u << 16); };
+            auto hi = [](uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); };
             *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) =
-                make_uint2(pack_bf2(v[0] * gelu_grad_sel(pu.x & 0xffff, gtb), v[1] * gelu_grad_sel(pu.x >> 16, gtb)),
-                           pack_bf2(v[2] * gelu_grad_sel(pu.y & 0xffff, gtb), v[3] * gelu_grad_sel(pu.y >> 16, gtb)));
+                make_uint2(pack_bf2(v[0] * lo(pu.x), v[1] * hi(pu.x)), pack_bf2(v[2] * lo(pu.y), v[3] * hi(pu.y)));
           }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);

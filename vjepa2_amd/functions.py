@@ -155,10 +155,11 @@ def block_forward(x, blk, lay, save):
     x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32_RESID, resid=x)
     ln2, m2, r2 = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, want_stats=save)
     hidden = mlp.fc1.weight.shape[0]
-    pre = torch.empty(T, hidden, dtype=BF16, device=x.device) if save else None
-    _, act = ops.linear_fwd(ln2, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=pre)
+    # the fc1 epilogue saves GELU'(pre-activation) for the backward (bf16, the bytes the pre-activation took)
+    dgelu = torch.empty(T, hidden, dtype=BF16, device=x.device) if save else None
+    _, act = ops.linear_fwd(ln2, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=dgelu)
     x_out = ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_F32_RESID, resid=x_mid)
-    saved = (x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, pre, act) if save else None
+    saved = (x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, dgelu, act) if save else None
     return x_out, saved
 
 
@@ -210,7 +211,7 @@ def _ln_grads(ln):
 
 
 def block_backward(dxo, blk, lay, saved):
-    x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, pre, act = saved
+    x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, dgelu, act = saved
     attn, mlp = blk.attn, blk.mlp
     T, D = x.shape
     H = attn.num_heads
@@ -218,7 +219,7 @@ def block_backward(dxo, blk, lay, saved):
     twin = getattr(dxo, "_vj_grad_bf16", None)  # bf16 twin written by the next block's LN1 backward,
     dxo_b = twin[0] if twin is not None and twin[1] == dxo._version else ops.cast_bf16(dxo)  # unless changed since
     # MLP
-    dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_pre=pre, wt=weight_bf16_t(mlp.fc2.weight))
+    dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
     ops.linear_wgrad(dxo_b, act, grad_buf(mlp.fc2.weight))  # fc2 bias grad: fused into LN2 backward
     dln2 = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
     ops.linear_wgrad(dpre, ln2, grad_buf(mlp.fc1.weight))
@@ -322,16 +323,16 @@ def attn_module_backward(dy, attn, lay, saved):
 def mlp_module_forward(x, mlp):
     """x bf16 [T, C] -> (fc2(GELU(fc1 x)) f32, saved)."""
     T = x.shape[0]
-    pre = torch.empty(T, mlp.fc1.weight.shape[0], dtype=BF16, device=x.device)
-    _, act = ops.linear_fwd(x, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=pre)
+    dgelu = torch.empty(T, mlp.fc1.weight.shape[0], dtype=BF16, device=x.device)
+    _, act = ops.linear_fwd(x, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=dgelu)
     y = ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_F32)
-    return y, (x, pre, act)
+    return y, (x, dgelu, act)
 
 
 def mlp_module_backward(dy, mlp, saved):
-    x, pre, act = saved
+    x, dgelu, act = saved
     dy_b = ops.cast_bf16(dy)
-    dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_pre=pre, wt=weight_bf16_t(mlp.fc2.weight))
+    dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
     ops.linear_wgrad(dy_b, act, grad_buf(mlp.fc2.weight))
     _bias_grad(mlp.fc2, dy)
     dx = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))

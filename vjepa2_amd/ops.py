@@ -119,7 +119,9 @@ def wgrad_splitk(M, N, K, cus=256):
 
 
 def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
-    """Y = X W^T + b.  x bf16 [M,K] row-major, w bf16 [N,K].  Returns the output tensor(s)."""
+    """Y = X W^T + b.  x bf16 [M,K] row-major, w bf16 [N,K].  Returns the output tensor(s).
+    EPI_GELU: (out, out2) = (GELU'(pre) bf16 if `out` is given (saved for the backward, EPI_GELU_BWD)
+    else None, GELU(pre) bf16), pre = the bf16-rounded X W^T + b."""
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K, (tuple(x.shape), tuple(w.shape))
@@ -140,15 +142,15 @@ def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
     return (out, out2) if epi == EPI_GELU else out
 
 
-def linear_dgrad(dy, w, out=None, gelu_pre=None, wt=None):
-    """dX = dY W (bf16 out); with gelu_pre: dX = (dY W) * GELU'(pre). `wt` = W^T [K, N] contiguous (the
+def linear_dgrad(dy, w, out=None, gelu_grad=None, wt=None):
+    """dX = dY W (bf16 out); with gelu_grad (the GELU derivative the forward's EPI_GELU saved): dX = (dY W) * gelu_grad. `wt` = W^T [K, N] contiguous (the
     K-major B operand the paired GEMM reads); without it W is read MN-major (256-row kernel)."""
     M, N = dy.shape
     K = w.shape[1]
     assert w.shape[0] == N
     out = out if out is not None else torch.empty(M, K, dtype=BF16, device=dy.device)
-    epi = EPI_GELU_BWD if gelu_pre is not None else EPI_BF16
-    aux = dict(aux=gelu_pre, ldaux=gelu_pre.stride(0) if gelu_pre is not None else 0)
+    epi = EPI_GELU_BWD if gelu_grad is not None else EPI_BF16
+    aux = dict(aux=gelu_grad, ldaux=gelu_grad.stride(0) if gelu_grad is not None else 0)
     if wt is not None:
         assert wt.shape == (K, N), (tuple(wt.shape), (K, N))
         gemm(M, K, N, dy, _rowmajor(dy, "dy"), True, wt, _rowmajor(wt, "wt"), True, epi, out=out, ldc=out.stride(0),

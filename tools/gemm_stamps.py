@@ -1,0 +1,43 @@
+"""Diagnostic: per-tile s_memtime stamps of k_gemm256 (build variant 'stamps', -DVJ_GEMM_STAMPS=1):
+main-loop and epilogue cycles per tile and how synchronised the CUs' epilogues are.
+usage: python tools/gemm_stamps.py [case-substring]"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import bench_kernels as bk  # noqa: E402
+
+lib = bk.load(os.path.join(bk.HERE, "vjepa2_amd", "libvjepa_hip_stamps.so"))
+dev = torch.device("cuda")
+stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+only = sys.argv[1] if len(sys.argv) > 1 else "tgt"
+for case in bk.GEMMS:
+    if only not in case[0]:
+        continue
+    run, fl = bk.gemm_case(lib, case, dev, stream)
+    run()
+    torch.cuda.synchronize()
+    lib.vj_debug_gemm_stamps_clear()
+    run()
+    torch.cuda.synchronize()
+    buf = np.zeros(2048 * 16 * 4, dtype=np.int64)
+    lib.vj_debug_gemm_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_long(buf.nbytes))
+    st = buf.reshape(2048, 16, 4)
+    valid = st[:, :, 0] != 0
+    main = (st[:, :, 1] - st[:, :, 0])[valid]
+    epi = (st[:, :, 2] - st[:, :, 1])[valid]
+    t0 = st[:, :, 0][valid].min()
+    end = st[:, :, 2][valid].max()
+    ntile = valid.sum(1)
+    print(f"{case[0]:22s} tiles/block {ntile[ntile > 0].min()}-{ntile.max()}  main {np.median(main):8.0f} cyc  "
+          f"epi {np.median(epi):8.0f} cyc (p10 {np.percentile(epi, 10):.0f} p90 {np.percentile(epi, 90):.0f})  "
+          f"span {end - t0} cyc", flush=True)
+    # epilogue start spread across blocks for tile 0 and 1
+    for it in range(2):
+        e1 = st[:, it, 1][st[:, it, 1] != 0]
+        if len(e1):
+            print(f"   tile {it}: epilogue starts spread {np.percentile(e1, 90) - np.percentile(e1, 10):.0f} cyc")

@@ -21,6 +21,10 @@
 #include <type_traits>
 #include "vj_common.h"
 
+// m-tiles of residual / saved-derivative rows the direct epilogue keeps in flight
+#ifndef VJ_GEMM_AUX_PF
+#define VJ_GEMM_AUX_PF 1
+#endif
 // Waves that issue the LDS-DMA of a K stage: 8 (all) or 4 (waves 0-3, so their SIMD partners 4-7
 // keep the matrix pipe busy while the DMA issues)
 #ifndef VJ_GEMM_DMA_WAVES
@@ -141,6 +145,10 @@ __device__ __forceinline__ uint32_t gelu_pair(uint32_t pk, uint32_t* dpk) {
   if (dpk) *dpk = pack_bf2(d0, d1);
   return pack_bf2(y0, y1);
 }
+
+#if VJ_GEMM_STAMPS  // diagnostic build: s_memtime per tile (start, main loop done, epilogue done) of wave 0
+__device__ long vj_gemm_stamps[2048 * 16 * 4];
+#endif
 
 struct Tile {
   int m0, n0, z, Keff, nk;  // buffer descriptors are rebuilt per DMA: SGPRs are the scarce resource
@@ -343,7 +351,13 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
     }
   };
 
+#if VJ_GEMM_STAMPS
+  int stamp_it = 0;
+#endif
   for (;;) {
+#if VJ_GEMM_STAMPS
+    const long st0 = __builtin_amdgcn_s_memtime();
+#endif
     const int wgn = wg + P;
     const bool has_next = wgn < runend;
     // the next tile's descriptors are rebuilt where they are used (SGPR pressure: 106 is the cap)
@@ -481,6 +495,9 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
     // the epilogue's lane-derived addressing is recomputed per tile (an opaque copy of the lane id
     // keeps the compiler from hoisting it out of the tile loop, where it would hold VGPRs across the
     // main loop)
+#if VJ_GEMM_STAMPS
+    const long st1 = __builtin_amdgcn_s_memtime();
+#endif
     int lane_e = lane;
     asm volatile("" : "+v"(lane_e));
 #if VJ_GEMM_NO_EPI  // measurement build: main loop only (the accumulators feed one never-taken store)
@@ -535,7 +552,11 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
         __syncthreads();
       }
       // residual (f32) / pre-activation (bf16 bits) rows: m-tile i+1's fetched while m-tile i is stored
-      [[maybe_unused]] float aux[2][4][NTN];
+      // AUX_PF m-tiles of rows in flight. Stamped (tools/gemm_stamps.py): the residual epilogue takes
+      // ~36k cycles per tile vs ~10k without the reads, but deeper prefetch (3, 5, 7) measured no
+      // faster: the 64 MB of residual every CU reads at once is the bound, not the latency chain
+      constexpr int AUX_PF = VJ_GEMM_AUX_PF;
+      [[maybe_unused]] float aux[AUX_PF + 1][4][NTN];
       auto fetch = [&](int i, float (&dst)[4][NTN]) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -589,15 +610,17 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
           }
         }
       };
-      if constexpr (AUX) fetch(0, aux[0]);
+      if constexpr (AUX)
+#pragma unroll
+        for (int i = 0; i < AUX_PF; ++i) fetch(i, aux[i]);
       // GELU: the derivative pass is compiled separately, for callers that save it (g.C)
       auto rows = [&](auto save_c) {
       constexpr bool SAVE_D = decltype(save_c)::value;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         if constexpr (AUX) {
-          if (i + 1 < 8) fetch(i + 1, aux[(i + 1) & 1]);
-          if (i == 6 && has_next) {  // behind the last aux fetch
+          if (i + AUX_PF < 8) fetch(i + AUX_PF, aux[(i + AUX_PF) % (AUX_PF + 1)]);
+          if (i == 7 - AUX_PF && has_next) {  // behind the last aux fetch
             const Tile nxt = make_tile(wgn);
             if (nxt.nk > 1) load_tile(nxt, 1, sle, lane);
           }
@@ -622,7 +645,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
             for (int e = 0; e < 4; ++e) {
               float x = acc[i][r][e];
               asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(bias[e]));
-              if constexpr (EPI == EPI_F32_RESID) asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(aux[i & 1][r][e]));
+              if constexpr (EPI == EPI_F32_RESID) asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(aux[i % (AUX_PF + 1)][r][e]));
               acc[i][r][e] = x;
             }
 #pragma unroll
@@ -660,7 +683,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
           }
           if constexpr (EPI == EPI_F32_RESID) {
 #pragma unroll
-            for (int j = 0; j < NTN; ++j) v[j] += aux[i & 1][r][j];
+            for (int j = 0; j < NTN; ++j) v[j] += aux[i % (AUX_PF + 1)][r][j];
           }
           if constexpr (F32OUT) {
             if (m < g.M && nok) {
@@ -675,7 +698,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
 #pragma unroll
             for (int q2 = 0; q2 < 2; ++q2) {
               if constexpr (EPI == EPI_GELU_BWD)
-                pk[r][q2] = pack_bf2(v[2 * q2] * aux[i & 1][r][2 * q2], v[2 * q2 + 1] * aux[i & 1][r][2 * q2 + 1]);
+                pk[r][q2] = pack_bf2(v[2 * q2] * aux[i % (AUX_PF + 1)][r][2 * q2],
+                                     v[2 * q2 + 1] * aux[i % (AUX_PF + 1)][r][2 * q2 + 1]);
               else
                 pk[r][q2] = pack_bf2(v[2 * q2], v[2 * q2 + 1]);
               if constexpr (EPI == EPI_GELU)  // pk: the bf16 pre-activation -> GELU, derivative (if saved)
@@ -804,6 +828,17 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
       }
     }
 
+#if VJ_GEMM_STAMPS
+    {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const long st2 = __builtin_amdgcn_s_memtime();
+      if (threadIdx.x == 0 && blockIdx.x < 2048 && stamp_it < 16) {
+        long* d = vj_gemm_stamps + ((long)blockIdx.x * 16 + stamp_it) * 4;
+        d[0] = st0; d[1] = st1; d[2] = st2; d[3] = __builtin_amdgcn_s_memrealtime();
+      }
+      ++stamp_it;
+    }
+#endif
     if (!has_next) break;
     wg = wgn;
     cur = make_tile(wgn);
@@ -1030,3 +1065,14 @@ extern "C" int vj_qkv_rope_gemm_fp8(int M, int K, const void* A, long lda, const
   return gemm256_f8(M, 3 * H * hd, K, A, lda, ea, B, ldb, eb, EPI_ROPE, bias, nullptr, 0, C, ldc, nullptr, 0,
                     (hipStream_t)stream, &rp);
 }
+
+#if VJ_GEMM_STAMPS
+extern "C" int vj_debug_gemm_stamps(void* dst, long nbytes) {
+  hipMemset(dst, 0, 0);
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(vj_gemm_stamps), nbytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+extern "C" int vj_debug_gemm_stamps_clear() {
+  static long z[2048 * 16 * 4];
+  return hipMemcpyToSymbol(HIP_SYMBOL(vj_gemm_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : 1;
+}
+#endif

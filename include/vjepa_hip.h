@@ -172,6 +172,15 @@ int vj_mask_count(int B, int duration, int height, int width, int npred, const i
 int vj_mask_emit(int B, int duration, int height, int width, int npred, const int* boxes, int t, int h, int w,
                  int max_ctx, int mode, int k_enc, int k_pred, long* enc, long* pred, void* stream);
 
+/* Video clip transform (app/vjepa/transforms.py:37-116 without auto-augment / motion shift /
+ * erasing): uint8 frames [B][T][H][W][C] -> f32 [B][C][T][S][S] = normalize(hflip(bilinear resize
+ * (crop))). params int32 [B][5] = (top, left, height, width, flip) from the host's draws (the
+ * reference's RNG order, video/transforms.py:470-507, :149-180); mean / stdv f32 [C] in uint8
+ * units (255 x the config's values). Replaces random_resized_crop + horizontal_flip +
+ * _tensor_normalize_inplace. */
+int vj_video_transform(int B, int T, int H, int W, int C, int S, const void* frames, const int* params,
+                       const float* mean, const float* stdv, float* out, void* stream);
+
 /* fp32-operand parity mode (vj_f32.hip): the encoder forward with f32 operands throughout, to show
  * the bf16 path's distance from the fp32 reference is operand rounding only. Not on the training
  * path. vj_gemm_f32: C = A B^T + bias (+ resid), epi as vj_gemm_bf16 (F32 = 1, F32_RESID = 2,

@@ -298,3 +298,21 @@ class OracleTrainer:
             for k in self.tgt:
                 ema_update(self.tgt[k], self.enc[k].detach(), momentum)
         return loss.item()
+
+
+# app/vjepa/transforms.py:98-112 with src/datasets/utils/video/transforms.py:510-542 (crop + bilinear
+# resize), :149-170 (flip) and transforms.py:139-152 (normalisation), for given draws
+def video_transform(buffer, params, crop, mean, std):
+    """buffer uint8 [T, H, W, C]; params (top, left, h, w, flip); mean / std per channel (0-1 units)."""
+    i, j, h, w, flip = params
+    x = buffer.to(torch.float32).permute(3, 0, 1, 2)  # C T H W
+    x = x[:, :, i:i + h, j:j + w]
+    x = F.interpolate(x, size=(crop, crop), mode="bilinear", align_corners=False)
+    if flip:
+        x = x.flip(-1)
+    m = torch.tensor(mean, dtype=torch.float32) * 255.0
+    s = torch.tensor(std, dtype=torch.float32) * 255.0
+    C, T, H, W = x.shape
+    x = x.reshape(C, -1).permute(1, 0)
+    x = (x - m) / s
+    return x.permute(1, 0).reshape(C, T, H, W)

@@ -34,6 +34,7 @@ SIGNATURES = {
     "vj_qkv_rope_gemm_fp8": [_I, _I, _P, _L, _P, _P, _L, _P, _P, _P, _L, _I, _I, _P, _I, _I, _I, _P, _P, _I, _P],
     "vj_quant_rows_fp8": [_I, _I, _P, _I, _L, _P, _L, _P, _P],
     "vj_layernorm_fwd_fp8": [_I, _I, _P, _I, _L, _P, _P, _F, _P, _L, _P, _P, _P, _P],
+    "vj_video_transform": [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P],
     "vj_mask_count": [_I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P],
     "vj_mask_emit": [_I, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "vj_gemm_f32": [_I, _I, _I, _P, _L, _P, _L, _I, _P, _P, _L, _P, _L, _P, _L, _P],

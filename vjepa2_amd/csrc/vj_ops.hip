@@ -1185,3 +1185,56 @@ extern "C" int vj_mask_emit(int B, int duration, int height, int width, int npre
   VJ_LAUNCH_CHECK("vj_mask_emit");
   return VJ_OK;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Video clip transform (app/vjepa/transforms.py:37-116, VideoTransform without auto-augment /
+// motion shift / random erasing): uint8 frames [B][T][H][W][C] -> f32 clips [B][C][T][S][S] =
+// normalize(hflip(bilinear_resize(crop))). The crop box and the flip come from the host's draws
+// (the reference's RNG calls, video/transforms.py:470-507 and :149-180); the resize is
+// F.interpolate(mode="bilinear", align_corners=False) (:537-542) with ATen's source-index rule
+// src = max((dst + 0.5) * in / out - 0.5, 0), idx1 = idx0 + (idx0 < in - 1), lambdas in f32; the
+// normalisation is (x - 255 mean_c) / (255 std_c) (:139-152). One thread per output element.
+namespace {
+
+__global__ void k_video_transform(long total, int T, int H, int W, int C, int S, const unsigned char* __restrict__ frames,
+                                  const int* __restrict__ params, const float* __restrict__ mean,
+                                  const float* __restrict__ stdv, float* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  const int x = (int)(e % S);
+  long r = e / S;
+  const int y = (int)(r % S);
+  r /= S;
+  const int t = (int)(r % T);
+  r /= T;
+  const int c = (int)(r % C);
+  const int b = (int)(r / C);
+  const int* p = params + 5 * b;  // top, left, height, width, flip
+  const int ci = p[0], cj = p[1], ch = p[2], cw = p[3];
+  const int xs = p[4] ? S - 1 - x : x;  // flip after the resize: read the mirrored output column
+  const float sh = (float)ch / (float)S, sw = (float)cw / (float)S;
+  const float fy = fmaxf(sh * ((float)y + 0.5f) - 0.5f, 0.f);
+  const float fx = fmaxf(sw * ((float)xs + 0.5f) - 0.5f, 0.f);
+  const int y0 = (int)fy, x0 = (int)fx;
+  const int y1 = y0 + (y0 < ch - 1 ? 1 : 0), x1 = x0 + (x0 < cw - 1 ? 1 : 0);
+  const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const unsigned char* f = frames + (((long)b * T + t) * H) * (long)W * C;
+  auto px = [&](int yy, int xx) { return (float)f[((long)(ci + yy) * W + (cj + xx)) * C + c]; };
+  const float v = ly0 * (lx0 * px(y0, x0) + lx1 * px(y0, x1)) + ly1 * (lx0 * px(y1, x0) + lx1 * px(y1, x1));
+  out[e] = (v - mean[c]) / stdv[c];
+}
+
+}  // namespace
+
+extern "C" int vj_video_transform(int B, int T, int H, int W, int C, int S, const void* frames, const int* params,
+                                  const float* mean, const float* stdv, float* out, void* stream) {
+  if (B == 0) return VJ_OK;
+  VJ_CHECK_ARG(B > 0 && T > 0 && H > 0 && W > 0 && C > 0 && S > 0 && frames && params && mean && stdv && out,
+               "vj_video_transform: bad arguments");
+  const long total = (long)B * C * T * S * S;
+  hipLaunchKernelGGL(k_video_transform, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     total, T, H, W, C, S, (const unsigned char*)frames, params, mean, stdv, out);
+  VJ_LAUNCH_CHECK("vj_video_transform");
+  return VJ_OK;
+}

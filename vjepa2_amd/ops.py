@@ -536,3 +536,16 @@ def mask_emit(B, duration, height, width, npred, boxes, t, h, w, max_ctx, mode, 
     assert enc.dtype == torch.int64 and pred.dtype == torch.int64 and enc.is_contiguous() and pred.is_contiguous()
     _call("vj_mask_emit", B, duration, height, width, npred, _p(boxes), t, h, w, max_ctx, mode, k_enc, k_pred,
           _p(enc), _p(pred), _stream())
+
+
+def video_transform(frames, params, crop, mean, std, out):
+    """uint8 frames [B, T, H, W, C] + per-clip (top, left, h, w, flip) int32 [B, 5] -> out f32 [B, C, T, S, S]."""
+    _dev(frames, params, mean, std, out)
+    assert frames.dtype == torch.uint8 and frames.is_contiguous() and frames.dim() == 5
+    B, T, H, W, C = frames.shape
+    assert params.dtype == torch.int32 and params.shape == (B, 5) and params.is_contiguous()
+    assert out.shape == (B, C, T, crop, crop) and out.dtype == F32 and out.is_contiguous()
+    p = params.cpu()
+    assert bool(((p[:, 2] > 0) & (p[:, 3] > 0) & (p[:, 0] >= 0) & (p[:, 1] >= 0) & (p[:, 0] + p[:, 2] <= H)
+                 & (p[:, 1] + p[:, 3] <= W)).all()), "crop boxes must lie inside the frames"
+    _call("vj_video_transform", B, T, H, W, C, crop, _p(frames), _p(params), _p(mean), _p(std), _p(out), _stream())

@@ -82,7 +82,9 @@ def main():
     from vjepa2_amd.train import JEPATrainer, init_opt, init_video_model
     import torch.distributed as dist
 
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    # one rank per GPU: the device is LOCAL_RANK (modulo the device count only when rehearsing several
+    # ranks on one device with VJ_DIST_BACKEND=gloo)
+    local_rank = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     world, rank = init_distributed()
     dev = torch.device("cuda", local_rank)

@@ -35,8 +35,8 @@ def init_distributed(port=37129, rank_and_world_size=(None, None), backend=None)
     if world == 1:
         return 1, 0
     os.environ.setdefault("MASTER_PORT", str(port))
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # VJ_DIST_BACKEND=gloo: rehearse several ranks on one device (RCCL refuses that)
+        backend = os.environ.get("VJ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     kw = {}
     if backend == "nccl" and torch.cuda.is_available():
         # the caller has bound this rank's GPU (torch.cuda.set_device(LOCAL_RANK)); RCCL connects

@@ -295,6 +295,42 @@ __global__ __launch_bounds__(1024) void k_colsum2(int S, int N, const float* __r
   }
 }
 
+// k_colsum2 for up to 4 column-sum vectors of one partial slab in ONE launch (the LayerNorm
+// backward's dgamma / dbeta / bias-gradient sums): blockIdx.y = vector k, partial rows of stride
+// ws_ld, vector k at column offset k * N; vectors with a null output are skipped.
+struct ColsumOuts {
+  float* out[4];
+};
+__global__ __launch_bounds__(1024) void k_colsum2_multi(int S, int N, const float* __restrict__ ws, long ws_ld,
+                                                        ColsumOuts outs) {
+  __shared__ float red[32][33];
+  float* out = outs.out[blockIdx.y];
+  if (out == nullptr) return;  // uniform per block
+  const float* w = ws + (long)blockIdx.y * N;
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int n = blockIdx.x * 32 + c;
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (n < N) {
+    int i = rg;
+    for (; i + 7 * 32 < S; i += 8 * 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = w[(long)(i + u * 32) * ws_ld + n];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s4[u & 3] += v[u];
+    }
+    for (int u = 0; i < S; i += 32, ++u) s4[u & 3] += w[(long)i * ws_ld + n];
+  }
+  red[rg][c] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  __syncthreads();
+  if (rg == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 32; ++r) t += red[r][c];
+    out[n] += t;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // RoPE on q and k of a [T, ld] bf16 qkv buffer, in place. Per head: three rotated slices of width
 // sw = 2*((hd/3)/2) (depth, height, width positions), rest untouched. Element j of a slice uses
@@ -793,11 +829,9 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
 #undef LNB
   VJ_LAUNCH_CHECK("vj_layernorm_bwd");
   // partials laid out [nb][nsum][D]: column k sums over rows of stride nsum*D
-  float* outs[4] = {dgamma, dbeta, sum_in, sum_out};
-  for (int k = 0; k < nsum; ++k) {
-    if (!outs[k]) continue;
-    hipLaunchKernelGGL(k_colsum2, dim3((D + 31) / 32), dim3(1024), 0, st, nb, D, ws + (long)k * D, (long)nsum * D,
-                       outs[k], nullptr, D, 1);
+  if (nsum) {  // every requested vector in one launch (same fixed-order sums as one launch each)
+    ColsumOuts o{{dgamma, dbeta, nsum > 2 ? sum_in : nullptr, nsum > 2 ? sum_out : nullptr}};
+    hipLaunchKernelGGL(k_colsum2_multi, dim3((D + 31) / 32, nsum), dim3(1024), 0, st, nb, D, ws, (long)nsum * D, o);
   }
   VJ_LAUNCH_CHECK("vj_layernorm_bwd(reduce)");
   return VJ_OK;

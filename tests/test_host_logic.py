@@ -42,6 +42,49 @@ def test_mask_options_bit_exact():
         assert torch.equal(e[0], ex["enc"][0]) and torch.equal(p[0], ex["pred"][0]), name
 
 
+def _np_build(spec):
+    """CPU restatement of vj_mask_count / vj_mask_emit (mode 0) for one MaskSpec."""
+    import numpy as np
+
+    D, H, W = spec.grid
+    t, h, w = spec.size
+    kept = []
+    for b in range(spec.boxes.shape[0]):
+        g = np.ones((D, H, W), bool)
+        g[spec.max_ctx:] = False
+        for s_, tp, lf in spec.boxes[b]:
+            g[s_:s_ + t, tp:tp + h, lf:lf + w] = False
+        kept.append(g.ravel())
+    ke = min(int(k.sum()) for k in kept)
+    kp = min(int((~k).sum()) for k in kept)
+    if spec.max_keep is not None:
+        ke = min(ke, spec.max_keep)
+    return (torch.tensor(np.stack([np.nonzero(k)[0][:ke] for k in kept])),
+            torch.tensor(np.stack([np.nonzero(~k)[0][:kp] for k in kept])))
+
+
+@pytest.mark.parametrize("extra", [{}, dict(max_temporal_keep=0.5, temporal_scale=[0.5, 1.0]), dict(max_keep=300)])
+def test_device_mask_draws_match_host_collate(extra):
+    """The device-mask collate (MaskCollator(device_masks=True)) makes exactly the host collate's RNG
+    draws: the masks rebuilt on the CPU from its MaskSpecs equal the host masks, and the global RNG
+    ends in the same state."""
+    from vjepa2_amd.masks import MaskCollator
+
+    cfgs = [dict(c, **extra) for c in VITL]
+    for seed in range(4):
+        host = MaskCollator(cfgs, [16], crop_size=256, patch_size=16)
+        dev = MaskCollator(cfgs, [16], crop_size=256, patch_size=16, device_masks=True)
+        torch.manual_seed(seed)
+        (_, he, hp), = host([(0, 0, [torch.arange(16)])] * 24)
+        after = torch.rand(1)
+        torch.manual_seed(seed)
+        (_, specs, none), = dev([(0, 0, [torch.arange(16)])] * 24)
+        assert none is None and torch.equal(torch.rand(1), after)
+        for j, spec in enumerate(specs):
+            e, p = _np_build(spec)
+            assert torch.equal(e, he[j]) and torch.equal(p, hp[j])
+
+
 def test_masks_are_sorted_disjoint():
     from vjepa2_amd.masks import MaskCollator
 

@@ -113,3 +113,24 @@ def test_train_steps_golden():
         close(tr.pred[k], v, 1e-6, f"final pred {k}")
     for k, v in g["final_target"].items():
         close(tr.tgt[k], v, 1e-6, f"final target {k}")
+
+
+def test_rope_angle_precision_envelope():
+    """The documented RoPE deviation, pinned as an envelope: the reference rotates q / k under
+    autocast, so modules.py:26-50 computes its angles in bf16 (x.dtype); the build uses fp32 angles
+    (reference op order). On ViT-L positions (frame < 8, row / col < 16, slice width 20) against
+    fp64 angles: the build's rotation is within bf16 output rounding of the exact one, the
+    reference's bf16-angle rotation is measurably further, and the two differ by at most 2.5e-2 of
+    max |x| (the reference's own angle error, up to ~8e-3 rad at these positions)."""
+    torch.manual_seed(0)
+    x = torch.randn(1, 1, 16, 20, dtype=torch.float64)
+    pos = torch.arange(16, dtype=torch.float64)[None, None]
+    exact = orc.rotate_queries_or_keys(x, pos)
+    ours = orc.rotate_queries_or_keys(x.float(), pos.float()).to(torch.bfloat16).double()
+    ref_autocast = orc.rotate_queries_or_keys(x.to(torch.bfloat16), pos.to(torch.bfloat16)).double()
+    scale = x.abs().max().item()
+    e_ours = (ours - exact).abs().max().item() / scale
+    e_ref = (ref_autocast - exact).abs().max().item() / scale
+    dev = (ours - ref_autocast).abs().max().item() / scale
+    print(f"RoPE vs fp64: fp32 angles {e_ours:.2e}, reference bf16 angles {e_ref:.2e}; deviation {dev:.2e}")
+    assert e_ours <= 2 ** -8 and e_ref > e_ours and dev <= 2.5e-2

@@ -181,6 +181,22 @@ int vj_mask_emit(int B, int duration, int height, int width, int npred, const in
 int vj_video_transform(int B, int T, int H, int W, int C, int S, const void* frames, const int* params,
                        const float* mean, const float* stdv, float* out, void* stream);
 
+/* Cross-attention of nq learned queries over N tokens (frozen-encoder probe: CrossAttention.forward,
+ * src/models/utils/modules.py:577-594 = F.scaled_dot_product_attention(q, k, v) with q [B, H, nq, hd],
+ * k / v [B, H, N, hd]; used by CrossAttentionBlock :606-610 and AttentivePooler attentive_pooler.py:91-100).
+ * q bf16 [B*nq][ldq] (head h at column h*hd), kv bf16 [B*N][ldkv] (k at h*hd, v at H*hd + h*hd: the
+ * reference's kv Linear output reshaped (B, N, 2, H, hd)), o bf16 [B*nq][ldo]; lse2 f32 [B*H][nq] =
+ * log2-domain log-sum-exp of scale*log2(e)*q.k, kept for the backward. hd % 8 == 0, hd <= 128.
+ * ws: f32 workspace of vj_xattn_ws_floats() floats (split-KV partials, 128 keys per chunk). */
+int vj_xattn_ws_floats(int B, int nq, int N, int H, int hd, long* out);
+int vj_xattn_fwd(int B, int nq, int N, int H, int hd, const void* q, long ldq, const void* kv, long ldkv, void* o,
+                 long ldo, float* lse2, float scale, float* ws, long ws_floats, void* stream);
+/* SDPA backward of vj_xattn_fwd (nq <= 16): dq bf16 [B*nq][lddq], dkv bf16 [B*N][lddkv] (dk | dv, same
+ * layout as kv, every element written). Deterministic: dq's cross-chunk sum is fixed-order. */
+int vj_xattn_bwd(int B, int nq, int N, int H, int hd, const void* q, long ldq, const void* kv, long ldkv,
+                 const void* o, long ldo, const void* dout, long lddo, const float* lse2, float scale, void* dq,
+                 long lddq, void* dkv, long lddkv, float* ws, long ws_floats, void* stream);
+
 /* fp32-operand parity mode (vj_f32.hip): the encoder forward with f32 operands throughout, to show
  * the bf16 path's distance from the fp32 reference is operand rounding only. Not on the training
  * path. vj_gemm_f32: C = A B^T + bias (+ resid), epi as vj_gemm_bf16 (F32 = 1, F32_RESID = 2,

@@ -316,3 +316,74 @@ def video_transform(buffer, params, crop, mean, std):
     x = x.reshape(C, -1).permute(1, 0)
     x = (x - m) / s
     return x.permute(1, 0).reshape(C, T, H, W)
+
+
+# ------------------------------------------------------------------------------------------------
+# Frozen-encoder consumers
+
+
+# src/models/utils/modules.py:566-594 (CrossAttention: q / kv Linears, SDPA, no output projection)
+def cross_attention(q, x, sd, prefix, num_heads):
+    B, n, C = q.shape
+    N = x.shape[1]
+    hd = C // num_heads
+    qh = F.linear(q, sd[prefix + "q.weight"], sd.get(prefix + "q.bias"))
+    qh = qh.reshape(B, n, num_heads, hd).permute(0, 2, 1, 3)
+    kv = F.linear(x, sd[prefix + "kv.weight"], sd.get(prefix + "kv.bias"))
+    kv = kv.reshape(B, N, 2, num_heads, hd).permute(2, 0, 3, 1, 4)
+    o = F.scaled_dot_product_attention(qh, kv[0], kv[1])
+    return o.transpose(1, 2).reshape(B, n, C)
+
+
+# src/models/utils/modules.py:597-610 (CrossAttentionBlock: norm1 is applied to the KEYS' input x)
+def cross_attention_block(q, x, sd, prefix, num_heads, eps=1e-5):
+    D = q.shape[-1]
+    xn = F.layer_norm(x, (D,), sd[prefix + "norm1.weight"], sd[prefix + "norm1.bias"], eps)
+    q = q + cross_attention(q, xn, sd, prefix + "xattn.", num_heads)
+    y = F.layer_norm(q, (D,), sd[prefix + "norm2.weight"], sd[prefix + "norm2.bias"], eps)
+    y = F.gelu(F.linear(y, sd[prefix + "mlp.fc1.weight"], sd[prefix + "mlp.fc1.bias"]))
+    return q + F.linear(y, sd[prefix + "mlp.fc2.weight"], sd[prefix + "mlp.fc2.bias"])
+
+
+# src/models/attentive_pooler.py:91-100 (depth-1 self-attention Blocks without RoPE, then the queries)
+def attentive_pooler(x, sd, prefix, num_heads, depth, complete_block=True, eps=1e-5):
+    for i in range(depth - 1):
+        x = block(x, sd, f"{prefix}blocks.{i}.", num_heads, eps=eps, use_rope=False)
+    q = sd[prefix + "query_tokens"].repeat(len(x), 1, 1)
+    if complete_block:
+        return cross_attention_block(q, x, sd, prefix + "cross_attention_block.", num_heads, eps)
+    return cross_attention(q, x, sd, prefix + "cross_attention_block.", num_heads)
+
+
+# src/models/attentive_pooler.py:134-137
+def attentive_classifier(x, sd, num_heads, depth, complete_block=True, eps=1e-5):
+    x = attentive_pooler(x, sd, "pooler.", num_heads, depth, complete_block, eps).squeeze(1)
+    return F.linear(x, sd["linear.weight"], sd["linear.bias"])
+
+
+# evals/video_classification_frozen/modelcustom/vit_encoder_multiclip.py:117-162 (ClipAggregation)
+def clip_aggregation(x, encode, tubelet_size, pos_embed=None, clip_indices=None):
+    """x: list (clips) of lists (views) of [B, C, F, H, W]; encode: clips -> [*, N, D] tokens;
+    pos_embed [1, max_T, D] or None. Returns a list (views) of [B, clips*T*S, D]."""
+    num_clips, num_views = len(x), len(x[0])
+    B, C, Fr, H, W = x[0][0].size()
+    outputs = encode(torch.cat([torch.cat(xi, dim=0) for xi in x], dim=0))
+    _, N, D = outputs.size()
+    T = Fr // tubelet_size
+    S = N // T
+    eff_B = B * num_views
+    views = [[] for _ in range(num_views)]
+    for i in range(num_clips):
+        o = outputs[i * eff_B:(i + 1) * eff_B]
+        for j in range(num_views):
+            views[j].append(o[j * B:(j + 1) * B])
+    res = []
+    for outs in views:
+        out = torch.cat([o.reshape(B, T, S, D) for o in outs], dim=1).flatten(1, 2)
+        if pos_embed is not None and clip_indices is not None:
+            idx = [c[:, ::tubelet_size] for c in clip_indices]
+            pe = pos_embed.repeat(B, 1, 1)
+            pe = torch.cat([apply_masks(pe, [i], concat=False)[0] for i in idx], dim=1)
+            out = out + pe.unsqueeze(2).repeat(1, 1, S, 1).flatten(1, 2)
+        res.append(out)
+    return res

@@ -398,6 +398,52 @@ def gen_resume():
                                wd=cap["wds"][3], after=cap["after"]))
 
 
+def gen_pooler():
+    """Frozen-encoder probe (src/models/attentive_pooler.py): an AttentiveClassifier (depth 3 = two
+    self-attention Blocks + the cross-attention block, 1 query, 10 classes) and a 3-query pooler
+    with the bare CrossAttention (complete_block=False); forward + backward on random tokens."""
+    from src.models.attentive_pooler import AttentiveClassifier, AttentivePooler
+
+    out = {}
+    for name, ctor, kw in (("clf", AttentiveClassifier, dict(embed_dim=64, num_heads=2, depth=3, num_classes=10)),
+                           ("pool3", AttentivePooler, dict(num_queries=3, embed_dim=64, num_heads=2, depth=2,
+                                                           complete_block=False))):
+        torch.manual_seed(11)
+        m = ctor(**kw)
+        init = {k: (v.double().sum().item(), v.double().pow(2).sum().item()) for k, v in m.state_dict().items()}
+        for p in m.parameters():  # non-trivial LN / bias / query values
+            with torch.no_grad():
+                p.add_(0.05 * torch.randn_like(p))
+        g = torch.Generator().manual_seed(12)
+        x = torch.randn(2, 40, 64, generator=g, requires_grad=True)
+        y = m(x)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy)
+        out[name] = dict(state={k: v.detach().clone() for k, v in m.state_dict().items()}, x=x.detach(),
+                         y=y.detach(), gy=gy, gx=x.grad.detach(), gparams=grads_of(m), cfg=kw, init=init)
+    save("pooler.pt", out)
+
+
+def gen_multiclip():
+    """ClipAggregation (evals/video_classification_frozen/modelcustom/vit_encoder_multiclip.py:87-162):
+    micro encoder, 2 clips x 2 views of 2 samples, temporal sincos pos-embed at the clips' frame indices."""
+    sys.path.insert(0, os.path.join(REF, "evals", "video_classification_frozen", "modelcustom"))
+    from vit_encoder_multiclip import ClipAggregation
+
+    torch.manual_seed(21)
+    enc = vit.VisionTransformer(img_size=32, patch_size=16, num_frames=4, tubelet_size=2, embed_dim=64, depth=2,
+                                num_heads=1, mlp_ratio=4, qkv_bias=True, use_rope=True, uniform_power=True,
+                                norm_layer=lambda d: torch.nn.LayerNorm(d, eps=1e-6))
+    agg = ClipAggregation(enc, tubelet_size=2, max_frames=16, use_pos_embed=True)
+    g = torch.Generator().manual_seed(22)
+    x = [[torch.randn(2, 3, 4, 32, 32, generator=g) for _ in range(2)] for _ in range(2)]
+    clip_indices = [torch.randint(0, 8, (2, 4), generator=g) for _ in range(2)]
+    with torch.no_grad():
+        outs = agg(x, clip_indices=clip_indices)
+    save("multiclip.pt", dict(state={k: v.clone() for k, v in enc.state_dict().items()}, x=x,
+                              clip_indices=clip_indices, outs=outs, pos_embed=agg.pos_embed.detach().clone()))
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # regenerate selected fixtures only: make_golden.py gen_main_vits gen_resume
         for name in sys.argv[1:]:
@@ -413,3 +459,5 @@ if __name__ == "__main__":
     gen_train_steps()
     gen_main_vits()
     gen_resume()
+    gen_pooler()
+    gen_multiclip()

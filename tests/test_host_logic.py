@@ -200,3 +200,19 @@ def test_step_flops_formula():
     mp = [torch.zeros(24, 966, dtype=torch.long), torch.zeros(24, 1437, dtype=torch.long)]
     f = step_flops("vit_large", 24, 2048, me, mp) / 24
     assert 3.4e12 < f < 3.7e12  # 3.56 TF/clip at the mean masks
+
+
+def test_pooler_init_matches_reference():
+    """AttentivePooler / AttentiveClassifier (attentive_pooler.py:16-137): same parameter names, shapes
+    and init RNG consumption as the reference (per-tensor sums of the reference's init, seed 11)."""
+    from vjepa2_amd.attentive_pooler import AttentiveClassifier, AttentivePooler
+
+    g = torch.load(os.path.join(os.path.dirname(__file__), "golden", "pooler.pt"), weights_only=True)
+    for which, ctor in (("clf", AttentiveClassifier), ("pool3", AttentivePooler)):
+        torch.manual_seed(11)
+        m = ctor(**g[which]["cfg"])
+        sd = m.state_dict()
+        assert set(sd) == set(g[which]["init"]), which
+        for k, (s1, s2) in g[which]["init"].items():
+            v = sd[k].double()
+            assert v.sum().item() == s1 and v.pow(2).sum().item() == s2, (which, k)

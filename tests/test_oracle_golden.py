@@ -134,3 +134,39 @@ def test_rope_angle_precision_envelope():
     dev = (ours - ref_autocast).abs().max().item() / scale
     print(f"RoPE vs fp64: fp32 angles {e_ours:.2e}, reference bf16 angles {e_ref:.2e}; deviation {dev:.2e}")
     assert e_ours <= 2 ** -8 and e_ref > e_ours and dev <= 2.5e-2
+
+
+@pytest.mark.parametrize("which", ["clf", "pool3"])
+def test_pooler_golden(which):
+    """Frozen-encoder probe (attentive_pooler.py / modules.py:566-610): the oracle's AttentiveClassifier
+    (2 Blocks + CrossAttentionBlock, 1 query) and 3-query AttentivePooler with the bare CrossAttention
+    reproduce the reference's outputs and every gradient."""
+    g = gold("pooler.pt")[which]
+    c = g["cfg"]
+    sd = {k: v.clone().requires_grad_(True) for k, v in g["state"].items()}
+    x = g["x"].clone().requires_grad_(True)
+    if which == "clf":
+        y = orc.attentive_classifier(x, sd, c["num_heads"], c["depth"])
+    else:
+        y = orc.attentive_pooler(x, sd, "", c["num_heads"], c["depth"], complete_block=c["complete_block"])
+    close(y, g["y"], 1e-5, f"{which} y")
+    y.backward(g["gy"])
+    close(x.grad, g["gx"], 1e-5, f"{which} dx")
+    assert set(g["gparams"]) <= set(sd)
+    for n, v in g["gparams"].items():
+        close(sd[n].grad, v, 1e-5, f"{which} d{n}")
+
+
+def test_multiclip_golden():
+    """ClipAggregation (vit_encoder_multiclip.py:117-162): clip / view regrouping, time-major
+    concatenation and the temporal sincos add at the clips' frame indices, vs the reference."""
+    g = gold("multiclip.pt")
+    sd = g["state"]
+    cfg = dict(patch_size=16, tubelet_size=2, num_heads=1, depth=2, use_rope=True)
+    t = torch.from_numpy(orc.sincos_1d(64, torch.arange(8).numpy().astype(float))).float()[None]
+    close(t, g["pos_embed"], 1e-7, "temporal sincos table")
+    outs = orc.clip_aggregation(g["x"], lambda c: orc.encoder_forward(c, sd, cfg), 2, g["pos_embed"],
+                                g["clip_indices"])
+    assert len(outs) == len(g["outs"])
+    for o, e in zip(outs, g["outs"]):
+        close(o, e, 1e-5, "multiclip view")

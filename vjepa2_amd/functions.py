@@ -462,8 +462,9 @@ def run_layernorm(x, ln, out_dtype=F32):
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, lin, out_dtype):
-        y = ops.linear_fwd(x, weight_bf16(lin.weight), lin.bias, EPI_BF16 if out_dtype == BF16 else EPI_F32)
-        ctx.lin, ctx.x = lin, x
+        xb = x.contiguous() if x.dtype == BF16 else ops.cast_bf16(x.contiguous())
+        y = ops.linear_fwd(xb, weight_bf16(lin.weight), lin.bias, EPI_BF16 if out_dtype == BF16 else EPI_F32)
+        ctx.lin, ctx.x, ctx.in_dtype = lin, xb, x.dtype
         return y
 
     @staticmethod
@@ -471,20 +472,21 @@ class _LinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         dy_b = dy if dy.dtype == BF16 else ops.cast_bf16(dy)
         lin = ctx.lin
-        dx = ops.linear_dgrad(dy_b, weight_bf16(lin.weight), wt=weight_bf16_t(lin.weight))
+        wt = weight_bf16_t(lin.weight) if lin.weight.shape[0] % 8 == 0 else None  # else padded in linear_dgrad
+        dx = ops.linear_dgrad(dy_b, weight_bf16(lin.weight), wt=wt)
         ops.linear_wgrad(dy_b, ctx.x, grad_buf(lin.weight))
         _bias_grad(lin, dy)
         ctx.x = None
         _fire_hook(lin)
-        return dx, None, None, None
+        return dx.to(ctx.in_dtype), None, None, None
 
 
 def run_linear(x, lin, out_dtype=F32):
-    """x bf16 [M, K] -> y [M, N] (out_dtype)."""
-    if x.dtype != BF16:
-        x = ops.cast_bf16(x.contiguous())
+    """x [M, K] (bf16, or f32: cast on the device; the gradient comes back in x's dtype) -> y [M, N]."""
     if _needs_grad(x, lin):
         return _LinearFn.apply(x, lin.weight, lin, out_dtype)
+    if x.dtype != BF16:
+        x = ops.cast_bf16(x.contiguous())
     return ops.linear_fwd(x, weight_bf16(lin.weight), lin.bias, EPI_BF16 if out_dtype == BF16 else EPI_F32)
 
 
@@ -533,3 +535,31 @@ def gather_rows(x, idx):
     if torch.is_grad_enabled() and x.requires_grad:
         return _GatherRowsFn.apply(x, idx)
     return ops.gather_rows(x, idx)
+
+
+# ------------------------------------------------------------------------------------------------
+# Cross-attention of learned queries over encoder tokens (modules.py:577-594 SDPA part)
+
+
+class _XAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, kv, B, nq, N, H, hd, scale):
+        o, lse2 = ops.xattn_fwd(q, kv, B, nq, N, H, hd, scale)
+        ctx.save_for_backward(q, kv, o, lse2)
+        ctx.dims = (B, nq, N, H, hd, scale)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, kv, o, lse2 = ctx.saved_tensors
+        do = do.contiguous()
+        do_b = do if do.dtype == BF16 else ops.cast_bf16(do.float())
+        dq, dkv = ops.xattn_bwd(q, kv, o, do_b, lse2, *ctx.dims)
+        return dq, dkv, None, None, None, None, None, None
+
+
+def cross_attention(q, kv, B, nq, N, H, hd, scale):
+    """q bf16 [B*nq, H*hd], kv bf16 [B*N, 2*H*hd] -> O bf16 [B*nq, H*hd] (SDPA, non-causal)."""
+    if torch.is_grad_enabled() and (q.requires_grad or kv.requires_grad):
+        return _XAttnFn.apply(q, kv, B, nq, N, H, hd, scale)
+    return ops.xattn_fwd(q, kv, B, nq, N, H, hd, scale)[0]

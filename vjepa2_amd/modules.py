@@ -144,6 +144,53 @@ class Block(nn.Module):
         return y.reshape(B, N, C)
 
 
+class CrossAttention(nn.Module):
+    """modules.py:566-594: q / kv Linears and SDPA of the (few) queries over the tokens x; no output
+    projection. q / kv projections on the HIP GEMMs (bf16 outputs), attention on vj_xattn."""
+
+    def __init__(self, dim, num_heads=12, qkv_bias=False, use_sdpa=True):
+        super().__init__()
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        self.scale = head_dim**-0.5
+        self.q = nn.Linear(dim, dim, bias=qkv_bias)
+        self.kv = nn.Linear(dim, int(dim * 2), bias=qkv_bias)
+        self.use_sdpa = use_sdpa
+        if head_dim % 8 or head_dim > 128:
+            raise NotImplementedError(f"HIP cross-attention supports head_dim % 8 == 0, <= 128 (got {head_dim})")
+
+    def forward(self, q, x):
+        """q [B, n, C], x [B, N, C] -> [B, n, C] (f32; SDPA's default scale = self.scale either branch)."""
+        B, n, C = q.shape
+        N = x.shape[1]
+        H = self.num_heads
+        qp = fn.run_linear(q.reshape(B * n, C), self.q, out_dtype=torch.bfloat16)
+        kv = fn.run_linear(x.reshape(B * N, C), self.kv, out_dtype=torch.bfloat16)
+        o = fn.cross_attention(qp, kv, B, n, N, H, C // H, self.scale)
+        return o.float().reshape(B, n, C)
+
+
+class CrossAttentionBlock(nn.Module):
+    """modules.py:597-610: q + xattn(q, norm1(x)); then q + mlp(norm2(q)). norm1 normalises the
+    TOKENS x (the keys / values), not the queries."""
+
+    def __init__(self, dim, num_heads, mlp_ratio=4.0, qkv_bias=False, act_layer=nn.GELU, norm_layer=nn.LayerNorm):
+        super().__init__()
+        self.norm1 = norm_layer(dim)
+        self.xattn = CrossAttention(dim, num_heads=num_heads, qkv_bias=qkv_bias)
+        self.norm2 = norm_layer(dim)
+        mlp_hidden_dim = int(dim * mlp_ratio)
+        self.mlp = MLP(in_features=dim, hidden_features=mlp_hidden_dim, act_layer=act_layer)
+
+    def forward(self, q, x):
+        B, n, C = q.shape
+        N = x.shape[1]
+        xn = fn.run_layernorm(x.reshape(B * N, C).contiguous(), self.norm1, out_dtype=torch.bfloat16)
+        q = q.float() + self.xattn(q, xn.reshape(B, N, C))
+        y = fn.run_layernorm(q.reshape(B * n, C).contiguous(), self.norm2, out_dtype=torch.bfloat16)
+        return q + fn.run_sublayer(y, self.mlp).reshape(B, n, C)
+
+
 def token_layout(B, N, mask, grid_size, H_patches, W_patches, device):
     """RoPE token positions of a [B, N] batch (modules.py:293-341): ids from `mask` ([B, N] token ids)
     or 0..N-1, split into (frame, row, col) by H_patches / W_patches or the init-time grid size."""

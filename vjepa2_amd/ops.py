@@ -148,6 +148,9 @@ def linear_dgrad(dy, w, out=None, gelu_grad=None, wt=None):
     M, N = dy.shape
     K = w.shape[1]
     assert w.shape[0] == N
+    if N % 8:  # the GEMM's K (= N here) must be a multiple of 8 (16-B DMA rows): zero-pad dY's columns
+        dy, w, wt = _pad_cols(dy), _pad_rows(w), None  # and W's rows (a classifier head's num_classes)
+        N = dy.shape[1]
     out = out if out is not None else torch.empty(M, K, dtype=BF16, device=dy.device)
     epi = EPI_GELU_BWD if gelu_grad is not None else EPI_BF16
     aux = dict(aux=gelu_grad, ldaux=gelu_grad.stride(0) if gelu_grad is not None else 0)
@@ -171,11 +174,29 @@ def transpose_bf16(x, out=None):
     return out
 
 
+def _pad_cols(t):
+    """[R, C] -> [R, C rounded up to 8], zero columns appended (GEMM operand rows are 16-B chunks)."""
+    out = torch.zeros(t.shape[0], (t.shape[1] + 7) // 8 * 8, dtype=t.dtype, device=t.device)
+    out[:, :t.shape[1]] = t
+    return out
+
+
+def _pad_rows(t):
+    out = torch.zeros((t.shape[0] + 7) // 8 * 8, t.shape[1], dtype=t.dtype, device=t.device)
+    out[:t.shape[0]] = t
+    return out
+
+
 def linear_wgrad(dy, x, dw):
     """dW[N,K] += dY^T X  (f32 accumulate into dw)."""
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dw.shape == (N, K) and dw.dtype == F32
+    if N % 8:  # dY^T is the MN-major A operand: its contiguous dim N must be a multiple of 8
+        tmp = torch.zeros((N + 7) // 8 * 8, K, dtype=F32, device=dw.device)
+        linear_wgrad(_pad_cols(dy), x, tmp)
+        dw += tmp[:N]
+        return dw
     gemm(N, K, M, dy, _rowmajor(dy, "dy"), False, x, _rowmajor(x, "x"), False, EPI_F32_RESID, out=dw,
          ldc=dw.stride(0), aux=dw, ldaux=dw.stride(0), splitk=wgrad_splitk(N, K, M))
     return dw
@@ -186,6 +207,14 @@ def colsum(x, out, accumulate=True):
     """out[n] (+)= sum_m x[m, n]; x bf16 or f32 [M,N]."""
     _dev(x, out)
     M, N = x.shape
+    if N % 8:  # 16-B row chunks: zero-pad the columns (a classifier head's bias gradient)
+        tmp = torch.zeros((N + 7) // 8 * 8, dtype=F32, device=x.device)
+        colsum(_pad_cols(x), tmp, accumulate=False)
+        if accumulate:
+            out += tmp[:N]
+        else:
+            out.copy_(tmp[:N])
+        return out
     S = min(256, max(1, (M + 63) // 64))
     ws = torch.empty(S * N, dtype=F32, device=x.device)
     _call("vj_colsum_f32", M, N, _p(x), int(x.dtype == BF16), _rowmajor(x, "x"), _p(out), int(accumulate), _p(ws),
@@ -327,6 +356,40 @@ def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None):
           int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), _stream(), label=f"attn_bwd<hd{hd}>",
           flops=sum(10.0 * n * l * l * D for n, l in groups))  # FA2 convention: 5 matmuls = 2.5 x forward
     return dqkv
+
+
+def _xattn_ws(B, nq, N, H, hd, device):
+    import ctypes
+
+    n = ctypes.c_long(0)
+    call("vj_xattn_ws_floats", B, nq, N, H, hd, ctypes.byref(n))
+    return torch.empty(max(1, n.value), dtype=F32, device=device)
+
+
+def xattn_fwd(q, kv, B, nq, N, H, hd, scale):
+    """Cross-attention (CrossAttention.forward's SDPA, modules.py:585-587): q bf16 [B*nq, H*hd],
+    kv bf16 [B*N, 2*H*hd] -> (O bf16 [B*nq, H*hd], lse2 f32 [B*H, nq])."""
+    _dev(q, kv)
+    assert q.dtype == BF16 and kv.dtype == BF16 and q.shape == (B * nq, H * hd) and kv.shape == (B * N, 2 * H * hd)
+    o = torch.empty(B * nq, H * hd, dtype=BF16, device=q.device)
+    lse2 = torch.empty(B * H, nq, dtype=F32, device=q.device)
+    ws = _xattn_ws(B, nq, N, H, hd, q.device)
+    _call("vj_xattn_fwd", B, nq, N, H, hd, _p(q), _rowmajor(q, "q"), _p(kv), _rowmajor(kv, "kv"), _p(o), H * hd,
+          _p(lse2), float(scale), _p(ws), ws.numel(), _stream(), label="xattn_fwd", flops=4.0 * B * nq * N * H * hd)
+    return o, lse2
+
+
+def xattn_bwd(q, kv, o, do, lse2, B, nq, N, H, hd, scale):
+    """Backward of xattn_fwd -> (dq bf16 [B*nq, H*hd], dkv bf16 [B*N, 2*H*hd])."""
+    _dev(q, kv, o, do, lse2)
+    assert do.dtype == BF16 and do.shape == o.shape
+    dq = torch.empty(B * nq, H * hd, dtype=BF16, device=q.device)
+    dkv = torch.empty(B * N, 2 * H * hd, dtype=BF16, device=q.device)
+    ws = _xattn_ws(B, nq, N, H, hd, q.device)
+    _call("vj_xattn_bwd", B, nq, N, H, hd, _p(q), _rowmajor(q, "q"), _p(kv), _rowmajor(kv, "kv"), _p(o),
+          _rowmajor(o, "o"), _p(do), _rowmajor(do, "do"), _p(lse2), float(scale), _p(dq), H * hd, _p(dkv), 2 * H * hd,
+          _p(ws), ws.numel(), _stream(), label="xattn_bwd", flops=10.0 * B * nq * N * H * hd)
+    return dq, dkv
 
 
 def qkv_rope(x, w, bias, H, hd, ids, ids_mod, tpf, tpr, cos_tab, sin_tab):

@@ -66,6 +66,16 @@ int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k
                 long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
                 const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
                 const float* cos_t, const float* sin_t, void* stream);
+/* Frame-causal (block-causal) variants for the action-conditioned predictor: with fblk > 0, token i
+ * of a sequence attends to key j iff j / fblk <= i / fblk, i.e. F.scaled_dot_product_attention with the
+ * attn_mask of build_action_block_causal_attention_mask (src/models/utils/modules.py:12-23; fblk = action
+ * tokens + H*W per frame, ACRoPEAttention.forward modules.py:243-247). fblk = 0 is vj_attn_fwd / _bwd. */
+int vj_attn_fwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o, long ldo,
+                   float* stats, float scale, int ngroups, const int* nseq, const int* len, int fblk, void* stream);
+int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, const void* o,
+                   long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
+                   const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
+                   const float* cos_t, const float* sin_t, int fblk, void* stream);
 
 /* Fused QKV projection + RoPE of q and k: C[M, 3*H*hd] (bf16) = A[M,K] W[3*H*hd, K]^T + bias, then
  * q, k columns rotated (modules.py:330 + 343-365) in the GEMM epilogue. Same RoPE arguments as vj_rope;

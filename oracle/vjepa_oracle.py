@@ -387,3 +387,95 @@ def clip_aggregation(x, encode, tubelet_size, pos_embed=None, clip_indices=None)
             out = out + pe.unsqueeze(2).repeat(1, 1, S, 1).flatten(1, 2)
         res.append(out)
     return res
+
+
+# ------------------------------------------------------------------------------------------------
+# V-JEPA 2-AC action-conditioned predictor
+
+
+# src/models/utils/modules.py:12-23
+def action_block_causal_mask(T, H, W, add_tokens=1):
+    n_t = add_tokens + H * W
+    mask = torch.zeros(T * n_t, T * n_t, dtype=torch.bool)
+    for t1 in range(T):
+        for t2 in range(0, t1 + 1):
+            mask[t1 * n_t:(t1 + 1) * n_t, t2 * n_t:(t2 + 1) * n_t] = True
+    return mask
+
+
+# src/models/utils/modules.py:163-258 (ACRoPEAttention.forward, mask=None)
+def ac_rope_attention(x, sd, prefix, num_heads, T, H, W, action_tokens, attn_mask, grid_size):
+    B, N, C = x.shape
+    hd = C // num_heads
+    sw = 2 * ((hd // 3) // 2)
+    ids = torch.arange(T * H * W)
+    d, h, w = (p.float() for p in separate_positions(ids, H * W, W))
+    h = h * (grid_size / H)
+    w = w * (grid_size / W)
+
+    def qkv_of(t):
+        return F.linear(t, sd[prefix + "qkv.weight"], sd[prefix + "qkv.bias"]).unflatten(
+            -1, (3, num_heads, hd)).permute(2, 0, 3, 1, 4)
+
+    xv = x.view(B, T, action_tokens + H * W, C)
+    aq, ak, av = [], [], []
+    for i in range(action_tokens):  # :183-200: depth slice rotated by the frame index, the rest as is
+        q, k, v = qkv_of(xv[:, :, i])
+        pos = torch.arange(T).float()
+        aq.append(torch.cat([rotate_queries_or_keys(q[..., :sw], pos), q[..., sw:]], -1))
+        ak.append(torch.cat([rotate_queries_or_keys(k[..., :sw], pos), k[..., sw:]], -1))
+        av.append(v)
+    q, k, v = qkv_of(xv[:, :, action_tokens:].flatten(1, 2))
+    qs, ks = [], []
+    for ax, pos in enumerate((d, h, w)):
+        qs.append(rotate_queries_or_keys(q[..., ax * sw:(ax + 1) * sw], pos))
+        ks.append(rotate_queries_or_keys(k[..., ax * sw:(ax + 1) * sw], pos))
+    q = torch.cat(qs + [q[..., 3 * sw:]], -1)
+    k = torch.cat(ks + [k[..., 3 * sw:]], -1)
+
+    def merge(tx, ta):  # :233-241: per frame, the action tokens first
+        tx = tx.reshape(B, num_heads, T, H * W, hd)
+        ta = torch.stack(ta, dim=3)  # [B, heads, T, A, hd]
+        return torch.cat([ta, tx], dim=3).flatten(2, 3)
+
+    if action_tokens > 0:
+        q, k, v = merge(q, aq), merge(k, ak), merge(v, av)
+    o = F.scaled_dot_product_attention(q, k, v, attn_mask=attn_mask)
+    o = o.transpose(1, 2).reshape(B, N, C)
+    return F.linear(o, sd[prefix + "proj.weight"], sd[prefix + "proj.bias"])
+
+
+# src/models/utils/modules.py:488-497 (ACBlock with ACRoPEAttention, GELU MLP)
+def ac_block(x, sd, prefix, num_heads, T, H, W, action_tokens, attn_mask, grid_size, eps=1e-6):
+    D = x.shape[-1]
+    y = F.layer_norm(x, (D,), sd[prefix + "norm1.weight"], sd[prefix + "norm1.bias"], eps)
+    x = x + ac_rope_attention(y, sd, prefix + "attn.", num_heads, T, H, W, action_tokens, attn_mask, grid_size)
+    y = F.layer_norm(x, (D,), sd[prefix + "norm2.weight"], sd[prefix + "norm2.bias"], eps)
+    y = F.gelu(F.linear(y, sd[prefix + "mlp.fc1.weight"], sd[prefix + "mlp.fc1.bias"]))
+    return x + F.linear(y, sd[prefix + "mlp.fc2.weight"], sd[prefix + "mlp.fc2.bias"])
+
+
+# src/models/ac_predictor.py:141-190
+def ac_predictor_forward(x, actions, states, sd, cfg, extrinsics=None, eps=1e-6):
+    gh = gw = cfg["grid"]
+    x = F.linear(x, sd["predictor_embed.weight"], sd["predictor_embed.bias"])
+    B, N_ctxt, D = x.shape
+    T = N_ctxt // (gh * gw)
+    s = F.linear(states, sd["state_encoder.weight"], sd["state_encoder.bias"]).unsqueeze(2)
+    a = F.linear(actions, sd["action_encoder.weight"], sd["action_encoder.bias"]).unsqueeze(2)
+    x = x.view(B, T, gh * gw, D)
+    if cfg["use_extrinsics"]:
+        e = F.linear(extrinsics, sd["extrinsics_encoder.weight"], sd["extrinsics_encoder.bias"]).unsqueeze(2)
+        x = torch.cat([a, s, e, x], dim=2).flatten(1, 2)
+    else:
+        x = torch.cat([a, s, x], dim=2).flatten(1, 2)
+    cond = 3 if cfg["use_extrinsics"] else 2
+    mask = None
+    if cfg["is_frame_causal"]:
+        mask = action_block_causal_mask(cfg["num_frames"] // cfg["tubelet_size"], gh, gw, cond)
+        mask = mask[:x.size(1), :x.size(1)]
+    for i in range(cfg["depth"]):
+        x = ac_block(x, sd, f"predictor_blocks.{i}.", cfg["num_heads"], T, gh, gw, cond, mask, gh, eps)
+    x = x.view(B, T, cond + gh * gw, D)[:, :, cond:].flatten(1, 2)
+    x = F.layer_norm(x, (D,), sd["predictor_norm.weight"], sd["predictor_norm.bias"], eps)
+    return F.linear(x, sd["predictor_proj.weight"], sd["predictor_proj.bias"])

@@ -444,6 +444,43 @@ def gen_multiclip():
                               clip_indices=clip_indices, outs=outs, pos_embed=agg.pos_embed.detach().clone()))
 
 
+def gen_ac_predictor():
+    """Action-conditioned predictor (src/models/ac_predictor.py:17-200): micro vit_ac_predictor
+    (2x2 patches per frame, 3 frames after tubelets, 2 blocks, head dim 32), frame-causal with and without
+    extrinsics; forward + backward."""
+    from src.models.ac_predictor import vit_ac_predictor
+    from src.models.utils.modules import build_action_block_causal_attention_mask
+
+    out = {}
+    for name, kw in (("causal", dict(use_extrinsics=False, is_frame_causal=True)),
+                     ("causal_ext", dict(use_extrinsics=True, is_frame_causal=True))):
+        # (is_frame_causal=False raises in the reference: ac_predictor.py:174 slices attn_mask = None)
+        cfg = dict(img_size=32, patch_size=16, num_frames=6, tubelet_size=2, embed_dim=96, predictor_embed_dim=64,
+                   depth=2, num_heads=2, action_embed_dim=7, **kw)
+        torch.manual_seed(31)
+        m = vit_ac_predictor(**cfg)
+        init = {k: (v.double().sum().item(), v.double().pow(2).sum().item()) for k, v in m.state_dict().items()}
+        for p in m.parameters():
+            with torch.no_grad():
+                p.add_(0.05 * torch.randn_like(p))
+        g = torch.Generator().manual_seed(32)
+        B, T = 2, 3
+        x = torch.randn(B, T * 4, 96, generator=g, requires_grad=True)
+        actions = torch.randn(B, T, 7, generator=g, requires_grad=True)
+        states = torch.randn(B, T, 7, generator=g, requires_grad=True)
+        ext = torch.randn(B, T, 6, generator=g, requires_grad=True)
+        y = m(x, actions, states, ext if kw["use_extrinsics"] else None)
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy)
+        out[name] = dict(state={k: v.detach().clone() for k, v in m.state_dict().items()}, x=x.detach(),
+                         actions=actions.detach(), states=states.detach(), ext=ext.detach(), y=y.detach(), gy=gy,
+                         gx=x.grad.detach(), gactions=actions.grad.detach(), gstates=states.grad.detach(),
+                         gext=ext.grad.detach() if kw["use_extrinsics"] else None, gparams=grads_of(m), cfg=cfg,
+                         init=init)
+    out["mask_T3_2x2_a2"] = build_action_block_causal_attention_mask(3, 2, 2, add_tokens=2)
+    save("ac_predictor.pt", out)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1:  # regenerate selected fixtures only: make_golden.py gen_main_vits gen_resume
         for name in sys.argv[1:]:
@@ -461,3 +498,4 @@ if __name__ == "__main__":
     gen_resume()
     gen_pooler()
     gen_multiclip()
+    gen_ac_predictor()

@@ -216,3 +216,22 @@ def test_pooler_init_matches_reference():
         for k, (s1, s2) in g[which]["init"].items():
             v = sd[k].double()
             assert v.sum().item() == s1 and v.pow(2).sum().item() == s2, (which, k)
+
+
+def test_ac_predictor_init_matches_reference():
+    """VisionTransformerPredictorAC (ac_predictor.py:17-139): parameter names, shapes and init RNG
+    consumption equal the reference's (per-tensor sums of its init, seed 31); the frame-causal mask
+    builder equals modules.py:12-23."""
+    from vjepa2_amd.ac_predictor import vit_ac_predictor
+    from vjepa2_amd.modules import build_action_block_causal_attention_mask
+
+    g = torch.load(os.path.join(os.path.dirname(__file__), "golden", "ac_predictor.pt"), weights_only=True)
+    assert torch.equal(build_action_block_causal_attention_mask(3, 2, 2, 2), g["mask_T3_2x2_a2"])
+    for which in ("causal", "causal_ext"):
+        torch.manual_seed(31)
+        m = vit_ac_predictor(**g[which]["cfg"])
+        sd = m.state_dict()
+        assert set(sd) == set(g[which]["init"]), which
+        for k, (s1, s2) in g[which]["init"].items():
+            v = sd[k].double()
+            assert v.sum().item() == s1 and v.pow(2).sum().item() == s2, (which, k)

@@ -170,3 +170,30 @@ def test_multiclip_golden():
     assert len(outs) == len(g["outs"])
     for o, e in zip(outs, g["outs"]):
         close(o, e, 1e-5, "multiclip view")
+
+
+@pytest.mark.parametrize("which", ["causal", "causal_ext"])
+def test_ac_predictor_golden(which):
+    """V-JEPA 2-AC predictor (ac_predictor.py:141-190, ACRoPEAttention modules.py:163-258): the oracle
+    reproduces the reference's output and every gradient (frame-causal mask, action / state /
+    extrinsics tokens)."""
+    g = gold("ac_predictor.pt")
+    assert torch.equal(orc.action_block_causal_mask(3, 2, 2, 2), g["mask_T3_2x2_a2"])
+    g = g[which]
+    c = g["cfg"]
+    cfg = dict(grid=c["img_size"] // c["patch_size"], use_extrinsics=c["use_extrinsics"],
+               is_frame_causal=c["is_frame_causal"], num_frames=c["num_frames"], tubelet_size=c["tubelet_size"],
+               depth=c["depth"], num_heads=c["num_heads"])
+    sd = {k: v.clone().requires_grad_(True) for k, v in g["state"].items()}
+    ins = {k: g[k].clone().requires_grad_(True) for k in ("x", "actions", "states", "ext")}
+    y = orc.ac_predictor_forward(ins["x"], ins["actions"], ins["states"], sd, cfg,
+                                 extrinsics=ins["ext"] if c["use_extrinsics"] else None)
+    close(y, g["y"], 1e-5, f"{which} y")
+    y.backward(g["gy"])
+    close(ins["x"].grad, g["gx"], 1e-5, "dx")
+    close(ins["actions"].grad, g["gactions"], 1e-5, "dactions")
+    close(ins["states"].grad, g["gstates"], 1e-5, "dstates")
+    if c["use_extrinsics"]:
+        close(ins["ext"].grad, g["gext"], 1e-5, "dext")
+    for n, v in g["gparams"].items():
+        close(sd[n].grad, v, 1e-5, f"{which} d{n}")

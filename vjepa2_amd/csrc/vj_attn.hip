@@ -73,7 +73,16 @@ struct AttnArgs {
   int rope_mod, rope_tpf, rope_tpr, rope_half;
   const float* cos_t;
   const float* sin_t;
+  // frame-causal (block-causal) mask: token i of a sequence attends to key j iff j / fblk <= i / fblk
+  // (build_action_block_causal_attention_mask, modules.py:12-23, with fblk = cond tokens + H*W);
+  // 0 = non-causal (every key of the sequence)
+  int fblk;
 };
+
+// key limit of query qloc (keys [0, klim) are visible) and its block-uniform bounds
+__device__ __forceinline__ int fc_klim(int fblk, int qloc, int len) {
+  return fblk ? min(len, (qloc / fblk + 1) * fblk) : len;
+}
 
 // padded head dim of the LDS images and MFMA loops
 template <int HD>
@@ -261,6 +270,11 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_
   const int qloc = qt * 128 + wave * 32 + (lane & 31);
   const bool qok = qloc < len;
   const int hl = lane >> 5;
+  // frame-causal: this lane's key limit; the block's keys end at its last query's limit, and tiles
+  // past its first query's limit take the per-lane mask (both = len when non-causal)
+  const int klim = fc_klim(a.fblk, qloc, len);
+  const int kend = fc_klim(a.fblk, min(qt * 128 + 127, len - 1), len);
+  const int kmask0 = fc_klim(a.fblk, qt * 128, len);
 
   // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[q][16s + 8h + j] (zero past HD).
   bf16x8 qf[HDP / 16];
@@ -290,7 +304,7 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_
   const float c = a.scale * LOG2E;
   const float tau = TAU / c;
 
-  const int nkt = (len + KT - 1) / KT;
+  const int nkt = (kend + KT - 1) / KT;
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
   stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
   __syncthreads();
@@ -328,13 +342,13 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_
 #pragma unroll
       for (int d = 0; d < HDP / 32; ++d) vf[ks][d] = tr_frag<HDP>(Vs, ks * 16, d * 32, lane);
     const int kb = kt * KT;
-    if (kb + KT > len) {  // ragged last tile only: keys beyond the sequence get -inf
+    if (kb + KT > kmask0) {  // ragged last tile (or frame-causal boundary tiles): keys past the limit get -inf
       asm volatile("");  // keeps the compiler from if-converting this into every tile
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (kb + kk * 32 + acc_row(r, lane) >= len) st[kk][r] = -INFINITY;
+          if (kb + kk * 32 + acc_row(r, lane) >= klim) st[kk][r] = -INFINITY;
     }
     float mx = st[0][0];
 #pragma unroll
@@ -485,7 +499,15 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   };
 
   const int nqt = (len + QT - 1) / QT;
-  stage(0, smem);
+  // frame-causal: key k is seen by queries from its frame block's start on; the sweep starts at the
+  // block's first key's frame start, and query tiles before its last key's frame start take the mask
+  int qlo[KW];
+#pragma unroll
+  for (int kw = 0; kw < KW; ++kw) qlo[kw] = a.fblk ? (min(kloc[kw], len - 1) / a.fblk) * a.fblk : 0;
+  const int kfirst = kt * 128 * KW, klast = min(kfirst + 128 * KW - 1, len - 1);
+  const int qt_first = a.fblk ? ((kfirst / a.fblk) * a.fblk) / QT : 0;
+  const int qmask_end = a.fblk ? (klast / a.fblk) * a.fblk : 0;  // tiles starting below this are masked
+  stage(qt_first, smem);
   __syncthreads();
   // Rows of queries past the sequence end are zero (DMA range check) with lse2 = delta = 0, so they
   // add exactly 0 to dV and dK; columns of keys past the end are never stored. No masks needed.
@@ -531,6 +553,14 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
         dtf[s2][d] = tr_frag<HDP>(Ds, s2 * 16, d * 32, lane);
         qtf[s2][d] = tr_frag<HDP>(Qs, s2 * 16, d * 32, lane);
       }
+    if (qt * QT < qmask_end) {  // frame-causal: queries of earlier frames than the key see nothing
+      asm volatile("");
+#pragma unroll
+      for (int kw = 0; kw < KW; ++kw)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (qt * QT + acc_row(r, lane) < qlo[kw]) sacc[kw][r] = -INFINITY;
+    }
     // P = 2^(c*S - lse2); dS = P * (dP - delta)
 #pragma unroll
     for (int kw = 0; kw < KW; ++kw)
@@ -561,7 +591,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       }
     __syncthreads();
   };
-  for (int qt0 = 0; qt0 < nqt; qt0 += 2) {
+  for (int qt0 = qt_first; qt0 < nqt; qt0 += 2) {
     tile_iter(qt0, std::integral_constant<int, 0>{});
     if (qt0 + 1 < nqt) tile_iter(qt0 + 1, std::integral_constant<int, 1>{});
   }
@@ -642,8 +672,15 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
   float nl2[QW];  // -lse2 / c: initial value of the S^T accumulators, so p = 2^(c * acc)
 #pragma unroll
   for (int qw = 0; qw < QW; ++qw) nl2[qw] = -lse2[qw] / c;
+  // frame-causal key limits (as in the forward)
+  int klim[QW];
+#pragma unroll
+  for (int qw = 0; qw < QW; ++qw) klim[qw] = fc_klim(a.fblk, qloc[qw], len);
+  const int q_first = qt * 128 * QW;
+  const int kend = fc_klim(a.fblk, min(q_first + 128 * QW - 1, len - 1), len);
+  const int kmask0 = fc_klim(a.fblk, q_first, len);
 
-  const int nkt = (len + KT - 1) / KT;
+  const int nkt = (kend + KT - 1) / KT;
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
   stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
   __syncthreads();
@@ -658,7 +695,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
       stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
       stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
     }
-    const bool ragged = (kt + 1) * KT > len;
+    const bool ragged = (kt + 1) * KT > kmask0;
     // Per 32-key half kk: S^T = K Q^T and dP^T - delta = V dO^T - delta for the QW query tiles, then
     // dQ^T += K^T dS^T. Halves run one after the other so only one half's fragments are live.
 #pragma unroll
@@ -696,7 +733,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
         for (int qw = 0; qw < QW; ++qw)
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            if (kt * KT + kk * 32 + acc_row(r, lane) >= len) st[qw][r] = -INFINITY;
+            if (kt * KT + kk * 32 + acc_row(r, lane) >= klim[qw]) st[qw][r] = -INFINITY;
       }
 #pragma unroll
       for (int qw = 0; qw < QW; ++qw)
@@ -777,13 +814,15 @@ int check_common(int H, int hd, long ld, long ldo) {
 
 }  // namespace
 
-extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o,
-                           long ldo, float* lse_stats, float scale, int ngroups, const int* nseq, const int* len,
-                           void* stream) {
+extern "C" int vj_attn_fwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                              void* o, long ldo, float* lse_stats, float scale, int ngroups, const int* nseq,
+                              const int* len, int fblk, void* stream) {
   if (T == 0) return VJ_OK;
   int rc = check_common(H, hd, ld, ldo);
   if (rc) return rc;
+  VJ_CHECK_ARG(fblk >= 0, "vj_attn_fwd: bad frame block %d", fblk);
   AttnArgs a{};
+  a.fblk = fblk;
   a.qkv = (const bf16_t*)qkv; a.ld = ld; a.q_off = q_off; a.k_off = k_off; a.v_off = v_off;
   a.o = (bf16_t*)o; a.ldo = ldo; a.stats = lse_stats; a.H = H; a.T = T; a.scale = scale;
   rc = fill_groups(a.sg, ngroups, nseq, len, 128, T);
@@ -800,14 +839,22 @@ extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q
   return VJ_OK;
 }
 
-extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
-                           const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
-                           float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
-                           int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t,
+extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o,
+                           long ldo, float* lse_stats, float scale, int ngroups, const int* nseq, const int* len,
                            void* stream) {
+  return vj_attn_fwd_fc(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, lse_stats, scale, ngroups, nseq, len, 0,
+                        stream);
+}
+
+extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                              const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
+                              long ldd, float scale, int ngroups, const int* nseq, const int* len,
+                              const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t,
+                              const float* sin_t, int fblk, void* stream) {
   if (T == 0) return VJ_OK;
   int rc = check_common(H, hd, ld, ldo);
   if (rc) return rc;
+  VJ_CHECK_ARG(fblk >= 0, "vj_attn_bwd: bad frame block %d", fblk);
   VJ_CHECK_ARG(lddo % 8 == 0 && ldd % 8 == 0, "vj_attn_bwd: strides must be multiples of 8");
   VJ_CHECK_ARG(!cos_t || (sin_t && (rope_ids || rope_mod > 0) && rope_tpf > 0 && rope_tpr > 0),
                "vj_attn_bwd: incomplete RoPE arguments");
@@ -821,7 +868,7 @@ extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q
   a.sin_t = sin_t;
   a.qkv = (const bf16_t*)qkv; a.ld = ld; a.q_off = q_off; a.k_off = k_off; a.v_off = v_off;
   a.o = (bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.stats = stats;
-  a.dqkv = (bf16_t*)dqkv; a.ldd = ldd; a.H = H; a.T = T; a.scale = scale;
+  a.dqkv = (bf16_t*)dqkv; a.ldd = ldd; a.H = H; a.T = T; a.scale = scale; a.fblk = fblk;
   // key / query 32-row tiles per wave of the two sweeps (block tile = 128 x that)
   const int kw = hd == 32 ? VJ_ATTN_KW32 : hd == 64 ? VJ_ATTN_KW64 : 1;
   const int qw = hd == 32 ? VJ_ATTN_QW32 : hd == 64 ? VJ_ATTN_QW64 : 1;
@@ -858,4 +905,13 @@ extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q
   }
   VJ_LAUNCH_CHECK("vj_attn_bwd");
   return VJ_OK;
+}
+
+extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                           const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
+                           float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
+                           int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t,
+                           void* stream) {
+  return vj_attn_bwd_fc(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
+                        nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, 0, stream);
 }

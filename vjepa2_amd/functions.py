@@ -98,7 +98,8 @@ class TokenLayout:
     """Ragged token batch: `groups` = [(nseq, seqlen), ...] in row order; RoPE ids per row
     (int32 device tensor) or None for `row % ids_mod`; tokens_per_frame / tokens_per_row."""
 
-    def __init__(self, groups, ids=None, ids_mod=0, tpf=1, tpr=1):
+    def __init__(self, groups, ids=None, ids_mod=0, tpf=1, tpr=1, fblk=0):
+        self.fblk = int(fblk)  # > 0: frame-causal attention over blocks of fblk tokens (AC predictor)
         self.groups = [(int(n), int(l)) for n, l in groups if n > 0]
         self.T = sum(n * l for n, l in self.groups)
         self.ids, self.ids_mod, self.tpf, self.tpr = ids, int(ids_mod), int(tpf), int(tpr)
@@ -131,7 +132,7 @@ def block_forward_fp8(x, blk, lay):
         qkv = ops.qkv_rope_fp8(ln1, e1, w8, ew, attn.qkv.bias, H, hd, lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
     else:
         qkv = ops.linear_fwd_fp8(ln1, e1, w8, ew, attn.qkv.bias, EPI_BF16)
-    o, _ = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd))
+    o, _ = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd), fblk=lay.fblk)
     x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32_RESID, resid=x)
     ln2, e2 = ops.layernorm_fwd_fp8(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
     w18, ew1 = weight_fp8(mlp.fc1.weight)
@@ -151,7 +152,7 @@ def block_forward(x, blk, lay, save):
                            lay.tpr, c, s)
     else:
         qkv = ops.linear_fwd(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
-    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd))
+    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd), fblk=lay.fblk)
     x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32_RESID, resid=x)
     ln2, m2, r2 = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, want_stats=save)
     hidden = mlp.fc1.weight.shape[0]
@@ -166,6 +167,8 @@ def block_forward(x, blk, lay, save):
 def block_forward_f32(x, blk, lay):
     """fp32-operand parity mode of block_forward: the same LayerNorm / RoPE kernels, f32 MFMA GEMMs
     (vj_gemm_f32) and exact-softmax attention (vj_attn_fwd_f32); every intermediate stays f32."""
+    if lay.fblk:
+        raise NotImplementedError("the fp32-operand parity mode has no frame-causal attention")
     attn, mlp = blk.attn, blk.mlp
     H = attn.num_heads
     hd = x.shape[1] // H
@@ -234,7 +237,7 @@ def block_backward(dxo, blk, lay, saved):
     if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
-    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope, fblk=lay.fblk)
     dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
     ops.linear_wgrad(dqkv, ln1, grad_buf(attn.qkv.weight))
     _bias_grad(attn.qkv, dqkv)
@@ -296,7 +299,7 @@ def attn_module_forward(x, attn, lay):
                            lay.tpr, c, s)
     else:
         qkv = ops.linear_fwd(x, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
-    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd))
+    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd), fblk=lay.fblk)
     y = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32)
     return y, (x, qkv, o, stats)
 
@@ -313,7 +316,7 @@ def attn_module_backward(dy, attn, lay, saved):
     if attn.use_rope:
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
-    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope, fblk=lay.fblk)
     dx = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
     ops.linear_wgrad(dqkv, x, grad_buf(attn.qkv.weight))
     _bias_grad(attn.qkv, dqkv)
@@ -472,7 +475,8 @@ class _LinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         dy_b = dy if dy.dtype == BF16 else ops.cast_bf16(dy)
         lin = ctx.lin
-        wt = weight_bf16_t(lin.weight) if lin.weight.shape[0] % 8 == 0 else None  # else padded in linear_dgrad
+        w = lin.weight
+        wt = weight_bf16_t(w) if w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 else None  # else padded in linear_dgrad
         dx = ops.linear_dgrad(dy_b, weight_bf16(lin.weight), wt=wt)
         ops.linear_wgrad(dy_b, ctx.x, grad_buf(lin.weight))
         _bias_grad(lin, dy)

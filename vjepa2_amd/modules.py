@@ -144,6 +144,94 @@ class Block(nn.Module):
         return y.reshape(B, N, C)
 
 
+def build_action_block_causal_attention_mask(T, H, W, add_tokens=1):
+    """modules.py:12-23: [N, N] bool, token i attends to j iff frame(j) <= frame(i), frames of
+    add_tokens + H*W tokens (local window = T: every earlier frame)."""
+    n_t = add_tokens + H * W
+    f = torch.arange(T * n_t) // n_t
+    return f[None, :] <= f[:, None]
+
+
+def ac_token_layout(B, T, H, W, cond, causal, device):
+    """TokenLayout of the action-conditioned sequence [B, T*(cond + H*W)] (ACRoPEAttention.forward,
+    modules.py:163-247): frame tokens keep their (frame, row, col) RoPE positions; each frame's cond
+    (action / state / extrinsics) tokens get id frame*H*W, i.e. position (frame, 0, 0): the depth slice
+    is rotated by the frame index and the row / column slices by angle 0 (= left unrotated, :190-193).
+    causal: frame-causal attention over blocks of cond + H*W tokens (the attn_mask of
+    build_action_block_causal_attention_mask)."""
+    hw = H * W
+    n_t = cond + hw
+    t = torch.arange(T, device=device)[:, None]
+    j = torch.arange(n_t, device=device)[None, :]
+    ids = torch.where(j < cond, t * hw, t * hw + (j - cond))  # [T, n_t]
+    ids = ids.reshape(1, -1).expand(B, -1).reshape(-1).to(torch.int32).contiguous()
+    return fn.TokenLayout([(B, T * n_t)], ids=ids, ids_mod=T * hw, tpf=hw, tpr=W, fblk=n_t if causal else 0)
+
+
+class ACRoPEAttention(RoPEAttention):
+    """modules.py:109-258 (same parameters as RoPEAttention; action tokens handled by the layout)."""
+
+    def forward(self, x, mask=None, attn_mask=None, T=None, H=None, W=None, action_tokens=0):
+        if mask is not None:
+            raise NotImplementedError("ACRoPEAttention with a token mask (the AC predictor passes None)")
+        B, N, C = x.shape
+        lay = _ac_layout_checked(B, N, attn_mask, T, H, W, action_tokens, self.grid_size, x.device)
+        return fn.run_sublayer(x.reshape(B * N, C), self, lay).reshape(B, N, C)
+
+
+def _ac_layout_checked(B, N, attn_mask, T, H, W, cond, grid_size, device):
+    if H != W or grid_size != H:
+        raise NotImplementedError("AC RoPE positions are snapped by grid_size / H, grid_size / W; only the "
+                                  "identity snap (square grid, grid_size == H) is on the HIP path")
+    n_t = cond + H * W
+    if T is None or N != T * n_t:
+        raise ValueError(f"AC sequence of {N} tokens is not T={T} frames of {n_t}")
+    causal = False
+    if attn_mask is not None:
+        ref = build_action_block_causal_attention_mask(T, H, W, cond)[:N, :N]
+        if not torch.equal(attn_mask.to(device="cpu", dtype=torch.bool), ref):
+            raise NotImplementedError("only the frame-causal attn_mask of build_action_block_causal_attention_mask "
+                                      "is supported on the HIP path")
+        causal = True
+    return ac_token_layout(B, T, H, W, cond, causal, device)
+
+
+class ACBlock(nn.Module):
+    """modules.py:432-497: the Block of the action-conditioned predictor (ACRoPEAttention or Attention)."""
+
+    def __init__(self, dim, num_heads, mlp_ratio=4.0, qkv_bias=False, qk_scale=None, drop=0.0, attn_drop=0.0,
+                 drop_path=0.0, act_layer=nn.GELU, wide_silu=True, norm_layer=nn.LayerNorm, use_sdpa=True,
+                 is_causal=False, grid_size=16, use_rope=False, **kwargs):
+        super().__init__()
+        self.norm1 = norm_layer(dim)
+        if use_rope:
+            self.attn = ACRoPEAttention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                                        attn_drop=attn_drop, use_sdpa=use_sdpa, is_causal=is_causal,
+                                        grid_size=grid_size, proj_drop=drop)
+        else:
+            self.attn = Attention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                                  attn_drop=attn_drop, use_sdpa=use_sdpa, is_causal=is_causal, proj_drop=drop)
+        if drop_path > 0.0:
+            raise NotImplementedError("stochastic depth (drop_path > 0) is not implemented (configs use 0)")
+        self.drop_path = nn.Identity()
+        self.norm2 = norm_layer(dim)
+        if act_layer is nn.SiLU:
+            raise NotImplementedError("SwiGLU MLP (use_silu) is not implemented on the HIP path (configs use GELU)")
+        self.mlp = MLP(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
+
+    def forward(self, x, mask=None, attn_mask=None, T=None, H=None, W=None, action_tokens=0):
+        if mask is not None:
+            raise NotImplementedError("ACBlock with a token mask (the AC predictor passes None)")
+        B, N, C = x.shape
+        if isinstance(self.attn, ACRoPEAttention):
+            lay = _ac_layout_checked(B, N, attn_mask, T, H, W, action_tokens, self.attn.grid_size, x.device)
+        else:
+            if attn_mask is not None:
+                raise NotImplementedError("attn_mask without RoPE is not on the AC predictor path")
+            lay = fn.TokenLayout([(B, N)], ids=None, ids_mod=N)
+        return fn.run_block(x.float().reshape(B * N, C).contiguous(), self, lay).reshape(B, N, C)
+
+
 class CrossAttention(nn.Module):
     """modules.py:566-594: q / kv Linears and SDPA of the (few) queries over the tokens x; no output
     projection. q / kv projections on the HIP GEMMs (bf16 outputs), attention on vj_xattn."""

@@ -125,6 +125,9 @@ def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K, (tuple(x.shape), tuple(w.shape))
+    if K % 8:  # 16-B operand rows: zero-pad the reduction dim (e.g. the 7-wide action / state encoders)
+        x, w = _pad_cols(x), _pad_cols(w)
+        K = x.shape[1]
     lda = _rowmajor(x, "x")
     ldb = _rowmajor(w, "w")
     if epi == EPI_BF16:
@@ -151,6 +154,9 @@ def linear_dgrad(dy, w, out=None, gelu_grad=None, wt=None):
     if N % 8:  # the GEMM's K (= N here) must be a multiple of 8 (16-B DMA rows): zero-pad dY's columns
         dy, w, wt = _pad_cols(dy), _pad_rows(w), None  # and W's rows (a classifier head's num_classes)
         N = dy.shape[1]
+    if K % 8:  # output width not a multiple of 8: compute into padded columns, return the view
+        assert gelu_grad is None and out is None
+        return linear_dgrad(dy, _pad_cols(w))[:, :K]
     out = out if out is not None else torch.empty(M, K, dtype=BF16, device=dy.device)
     epi = EPI_GELU_BWD if gelu_grad is not None else EPI_BF16
     aux = dict(aux=gelu_grad, ldaux=gelu_grad.stride(0) if gelu_grad is not None else 0)
@@ -196,6 +202,11 @@ def linear_wgrad(dy, x, dw):
         tmp = torch.zeros((N + 7) // 8 * 8, K, dtype=F32, device=dw.device)
         linear_wgrad(_pad_cols(dy), x, tmp)
         dw += tmp[:N]
+        return dw
+    if K % 8:  # X is the MN-major B operand: same for its width K
+        tmp = torch.zeros(N, (K + 7) // 8 * 8, dtype=F32, device=dw.device)
+        linear_wgrad(dy, _pad_cols(x), tmp)
+        dw += tmp[:, :K]
         return dw
     gemm(N, K, M, dy, _rowmajor(dy, "dy"), False, x, _rowmajor(x, "x"), False, EPI_F32_RESID, out=dw,
          ldc=dw.stride(0), aux=dw, ldaux=dw.stride(0), splitk=wgrad_splitk(N, K, M))
@@ -326,8 +337,9 @@ def rope_(qkv, H, hd, q_off, k_off, ids, ids_mod, tpf, tpr, cos_tab, sin_tab, in
          _p(cos_tab), _p(sin_tab), half, int(inverse), _stream())
 
 
-def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None):
-    """groups: list of (nseq, len). Returns (O bf16 [T, H*hd], stats f32 [2, H, T])."""
+def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None, fblk=0):
+    """groups: list of (nseq, len). Returns (O bf16 [T, H*hd], stats f32 [2, H, T]). fblk > 0: frame-causal
+    mask (token i sees key j iff j // fblk <= i // fblk)."""
     _dev(qkv)
     T = qkv.shape[0]
     D = H * hd
@@ -337,13 +349,13 @@ def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None):
     o = torch.empty(T, D, dtype=BF16, device=qkv.device)
     stats = torch.empty(2, H, T, dtype=F32, device=qkv.device)
     ns, ln = [g[0] for g in groups], [g[1] for g in groups]
-    _call("vj_attn_fwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, v_off, _p(o), D, _p(stats),
-          float(scale), len(groups), int_array(ns), int_array(ln), _stream(),
+    _call("vj_attn_fwd_fc", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, v_off, _p(o), D, _p(stats),
+          float(scale), len(groups), int_array(ns), int_array(ln), int(fblk), _stream(),
           label=f"attn_fwd<hd{hd}>", flops=sum(4.0 * n * l * l * D for n, l in groups))
     return o, stats
 
 
-def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None):
+def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None, fblk=0):
     """rope = (ids, ids_mod, tpf, tpr, cos_tab, sin_tab) -> dq, dk returned w.r.t. the un-rotated q, k."""
     _dev(qkv, o, do, stats)
     T = qkv.shape[0]
@@ -351,9 +363,10 @@ def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None):
     dqkv = dqkv if dqkv is not None else torch.empty(T, 3 * D, dtype=BF16, device=qkv.device)
     ns, ln = [g[0] for g in groups], [g[1] for g in groups]
     ids, mod, tpf, tpr, ct, st = rope if rope is not None else (None, 0, 0, 0, None, None)
-    _call("vj_attn_bwd", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
+    _call("vj_attn_bwd_fc", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
           _rowmajor(do, "do"), _p(stats), _p(dqkv), _rowmajor(dqkv, "dqkv"), float(scale), len(groups), int_array(ns),
-          int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), _stream(), label=f"attn_bwd<hd{hd}>",
+          int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), int(fblk), _stream(),
+          label=f"attn_bwd<hd{hd}>",
           flops=sum(10.0 * n * l * l * D for n, l in groups))  # FA2 convention: 5 matmuls = 2.5 x forward
     return dqkv
 

@@ -1026,12 +1026,23 @@ extern "C" int vj_ema(long n, float* target, const float* online, float momentum
   return VJ_OK;
 }
 
+// scalar elements [i0, n) of a cast whose length is not a multiple of 4 (tiny inputs, e.g. 7-wide actions)
+__global__ void k_cast_bf16_tail(long i0, long n, const float* __restrict__ in, bf16_t* __restrict__ out) {
+  const long i = i0 + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = f2bf(in[i]);
+}
+
 extern "C" int vj_cast_bf16(long n, const float* in, void* out, void* stream) {
   if (n == 0) return VJ_OK;
-  VJ_CHECK_ARG(n % 4 == 0, "vj_cast_bf16: n must be %%4");
-  const long n4 = n / 4;
-  hipLaunchKernelGGL(k_cast_bf16, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4,
-                     (const float4*)in, (uint2*)out);
+  VJ_CHECK_ARG(in && out, "vj_cast_bf16: null pointer");
+  const bool vec = !(((uintptr_t)in & 15) | ((uintptr_t)out & 7));
+  const long n4 = vec ? n / 4 : 0;
+  if (n4)
+    hipLaunchKernelGGL(k_cast_bf16, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4,
+                       (const float4*)in, (uint2*)out);
+  if (n4 * 4 < n)
+    hipLaunchKernelGGL(k_cast_bf16_tail, dim3(vj_cdiv(n - n4 * 4, 256)), dim3(256), 0, (hipStream_t)stream, n4 * 4, n,
+                       in, (bf16_t*)out);
   VJ_LAUNCH_CHECK("vj_cast_bf16");
   return VJ_OK;
 }

@@ -85,11 +85,12 @@ def test_gemm_splitk(epi, MNK):
     assert torch.equal(out, first), "split-K must be deterministic"
 
 
-@pytest.mark.parametrize("N", [256, 384, 200])
+@pytest.mark.parametrize("N", [256, 384, 200, 1152])
 @pytest.mark.parametrize("M", [333, 1333])
 def test_gemm_epilogues(M, N):
     """Every epilogue; M >= 1024 runs the 256-row kernel (N = 256: 256-wide tiles, 384 / 200: 128-wide,
-    200 ragged), whose K-major-B forms store straight from registers (permuted B staging)."""
+    200 ragged, 1152: 256-wide with a half-empty last column tile), whose K-major-B forms store straight
+    from registers (permuted B staging)."""
     from vjepa2_amd import ops
 
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -357,7 +358,7 @@ def test_rope_fwd_bwd(hd, H):
 
 
 @pytest.mark.parametrize("M", [300, 1500])
-@pytest.mark.parametrize("hd,H", [(64, 2), (32, 3), (80, 2), (88, 1)])
+@pytest.mark.parametrize("hd,H", [(64, 2), (32, 3), (80, 2), (88, 1), (32, 12)])
 def test_fused_rope_paths(M, hd, H):
     """QKV GEMM with RoPE fused into the epilogue vs fp32 GEMM + oracle RoPE (M >= 1024: one bf16
     rounding of the fp32 result, <= 1 ulp; M < 1024 takes GEMM -> bf16 -> rope -> bf16, two

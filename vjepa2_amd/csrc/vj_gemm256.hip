@@ -869,6 +869,13 @@ int stagger_units(int K) {
   return u > 0 ? (int)((long)u * K / 1024) : 0;
 }
 
+// VJ_GEMM_BN256=1 (experiment): 256-wide tiles (direct-store epilogue) also when N % 256 != 0, the
+// last column tile partly empty, instead of 128-wide tiles with the LDS-staged epilogue
+int force_bn256() {
+  const char* e = getenv("VJ_GEMM_BN256");
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
 int grid256(long nb) {
   int per_xcd = num_cus() / 8;
   const char* e = getenv("VJ_GEMM_PXCD");
@@ -942,7 +949,10 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
   if (epi < EPI_BF16 || epi > EPI_ROPE || N % 8 || ldc % 4 || ldc2 % 4 || ldaux % 4) return VJ_ERR_UNSUPPORTED;
   if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
     return VJ_ERR_UNSUPPORTED;
-  const int bn = (N % 256 == 0) ? 256 : 128;
+  // 256-wide tiles (direct-store epilogue) unless the last column tile would waste > 15 % of the work
+  // (measured, tools/bench_kernels.py: predictor QKV N = 1152 -17 % with 256-wide tiles; N = 384 +14 %)
+  const bool wide = N % 256 == 0 || (N > 256 && (vj_cdiv(N, 256) * 256L * 100 <= 115L * N || force_bn256()));
+  const int bn = wide ? 256 : 128;
   const int tm = vj_cdiv(M, 256), tn = vj_cdiv(N, bn);
   G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, C, ldc, C2, ldc2, bias, aux, ldaux,
          tm, tn, RopeP{}, K, 1, nullptr, tile_group(tm, tn)};

@@ -14,6 +14,9 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 
+_SHAPE_LABELS = bool(int(__import__("os").environ.get("VJ_SHAPE_LABELS", "0")))
+
+
 class KernelEvents:
     """Per-launch HIP-event timing of the library's kernels on the launching (current) stream,
     with the algorithmic FLOPs of each launch (bench.py roofline). Active only between start/stop."""
@@ -84,6 +87,8 @@ def gemm(M, N, K, a, lda, a_kmajor, b, ldb, b_kmajor, epi, out=None, ldc=0, out2
     if bias is not None and (bias.dtype != F32 or bias.numel() < N):
         raise TypeError("gemm bias must be f32 [N]")
     label = f"k_gemm<{int(a_kmajor)},{int(b_kmajor)},{EPI_NAMES[epi]}>"
+    if _SHAPE_LABELS:  # diagnostics (VJ_SHAPE_LABELS=1): per-shape kernel-event labels
+        label += f"[{M}x{N}x{K}]"
     if splitk > 1:  # same slicing as the library: kslice = ceil(ceil(K / splitk) / 64) * 64
         kslice = (K + splitk - 1) // splitk
         kslice = (kslice + 63) // 64 * 64

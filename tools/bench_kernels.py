@@ -62,6 +62,9 @@ GEMMS = [
     ("pred fc1", 71232, 1536, 384, 1, 1, 3, 1),
     ("pred fc1 save", 71232, 1536, 384, 1, 1, 7, 1),
     ("pred fc2", 71232, 384, 1536, 1, 1, 2, 1),
+    ("pred proj", 71232, 384, 384, 1, 1, 2, 1),
+    ("pred dgrad proj", 71232, 384, 384, 1, 1, 0, 1),
+    ("pred dgrad qkv", 71232, 384, 1152, 1, 1, 0, 1),
 ]
 
 

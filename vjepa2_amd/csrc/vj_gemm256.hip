@@ -82,22 +82,25 @@ __device__ __forceinline__ int mn_swz(int k) { return 2 * (k & 3) + 8 * ((k >> 3
 // group, so n-tile j of the MFMA accumulators covers the group's columns {NTN*c + j}: each lane
 // then owns NTN CONSECUTIVE output columns and the epilogue stores straight from registers.
 // NW waves issue the tile's 1-KB pieces (waves 0 .. NW-1).
-template <bool KMAJ, int ROWS, bool PERM = false, int NW = 8>
+template <bool KMAJ, int ROWS, bool PERM = false, int NW = 8, int BKT = 64, int WNX = 4>
 __device__ __forceinline__ void stage(__amdgpu_buffer_rsrc_t rs, long ld, int rows_left, int k0, int K,
                                       LDS_AS char* lds, int wave, int lane) {
-  constexpr int PIECES = ROWS / 8;  // 1-KB DMA pieces per operand tile
+  constexpr int PIECES = ROWS * BKT * 2 / 1024;  // 1-KB DMA pieces per operand tile
   constexpr int PPW = PIECES / NW;
+  static_assert(KMAJ || BKT == 64, "MN-major staging is written for 64-deep K tiles");
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     const int p = wave * PPW + i;
     uint32_t voff;
     if constexpr (KMAJ) {
-      const int r = p * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      // 128-B rows (BK 64): chunk ^= (row>>1)&7; 64-B rows (BK 32): chunk ^= (row>>2)&3
+      constexpr int CPR = BKT / 8, RPP = 64 / CPR;  // 16-B chunks per row, rows per piece
+      const int r = p * RPP + lane / CPR;
+      const int c = (lane % CPR) ^ (BKT == 64 ? ((r >> 1) & 7) : ((r >> 2) & 3));
       const int kk = k0 + c * 8;
       int gr = r;
       if constexpr (PERM) {
-        constexpr int WN = ROWS / 4, NTN = WN / 16;
+        constexpr int WN = ROWS / WNX, NTN = WN / 16;
         const int rl = r % WN;
         gr = (r - rl) + NTN * (rl & 15) + (rl >> 4);
       }
@@ -115,10 +118,14 @@ __device__ __forceinline__ void stage(__amdgpu_buffer_rsrc_t rs, long ld, int ro
 }
 
 // 16x16x32 operand fragment: lane l holds X(rb + (l&15), 32s + 8(l>>4) + j), j = 0..7.
-template <bool KMAJ, int ROWS>
+template <bool KMAJ, int ROWS, int BKT = 64>
 __device__ __forceinline__ bf16x8 frag(const LDS_AS char* lds, int rb, int s, int lane) {
   if constexpr (KMAJ) {
     const int r = rb + (lane & 15);
+    if constexpr (BKT == 32) {  // 64-B rows, one k-step
+      const int c = (lane >> 4) ^ ((r >> 2) & 3);
+      return *(const LDS_AS bf16x8*)(lds + r * 64 + c * 16);
+    }
     const int c = (4 * s + (lane >> 4)) ^ ((r >> 1) & 7);
     return *(const LDS_AS bf16x8*)(lds + r * 128 + c * 16);
   } else {
@@ -154,16 +161,23 @@ struct Tile {
   int m0, n0, z, Keff, nk;  // buffer descriptors are rebuilt per DMA: SGPRs are the scarce resource
 };
 
-template <bool AK, bool BKM, int EPI, int BN, bool F8 = false>
-__global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
+// NWV = 8: 8 waves (2 x 4), 64-deep K tiles, one workgroup per CU. NWV = 4 ("2W"): 4 waves (2 x 2),
+// 32-deep K tiles, 64 KB of LDS, TWO workgroups per CU, so one workgroup's epilogue (HBM / VALU)
+// runs under the other's main loop (MFMA); K-major operands only.
+template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8>
+__global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   static_assert(!F8 || (AK && BKM && EPI != EPI_PARTIAL && EPI != EPI_GELU_BWD), "fp8: forward GEMMs only");
+  static_assert(NWV == 8 || (NWV == 4 && AK && BKM && !F8), "2-workgroup GEMM: K-major bf16 operands only");
   constexpr int BM = 256;
+  constexpr int BK = NWV == 8 ? 64 : 32;
+  constexpr int NT = NWV * 64;
+  constexpr int WNX = NWV / 2;    // waves across N (4 / 2); 2 waves across M
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int WN = BN / 4;      // wave tile columns (64 / 32)
+  constexpr int WN = BN / WNX;    // wave tile columns (64 / 32)
   constexpr int NTN = WN / 16;    // 16-wide n tiles per wave (4 / 2)
-  constexpr int DMAW = VJ_GEMM_DMA_WAVES;
+  constexpr int DMAW = NWV == 8 ? VJ_GEMM_DMA_WAVES : NWV;
   // K-major B with 4 n-tiles per wave: permuted B staging + stores straight from registers (16-B
   // f32 / 8-B bf16 per row); 128-wide tiles would store 4-8 B per lane, so they keep the LDS path
   constexpr bool DIRECT = BKM && NTN == 4;
@@ -181,7 +195,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = wave / WNX, wc = wave % WNX;
 
   // Persistent walk. The logical tiles (K slice outermost, then the tile order) are cut into 8
   // contiguous runs, one per XCD (blocks b and b + 8 share an XCD); the P blocks of an XCD walk its
@@ -239,8 +253,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
                     int lane) {
     if (DMAW == 8 || wave < DMAW) {
       LDS_AS char* s = smem + slot * STAGE;
-      stage<AK, BM, false, DMAW>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
-      stage<BKM, BN, DIRECT, DMAW>(rb, g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, wave, lane);
+      stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
+      stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, wave, lane);
     }
   };
   auto load_tile = [&](const Tile& T, int t, int slot, int lane) {
@@ -249,13 +263,13 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
 
   // per-kernel tables (RoPE): global loads issued before the first DMA (so their waits do not queue
   // behind it), written to the table area after it; the first barrier of the tile loop publishes them
-  constexpr int RTR = EPI == EPI_ROPE ? (ROPE_TAB_MAX + 511) / 512 : 0;
+  constexpr int RTR = EPI == EPI_ROPE ? (ROPE_TAB_MAX + NT - 1) / NT : 0;
   [[maybe_unused]] f32x2 rpf[RTR > 0 ? RTR : 1];
   [[maybe_unused]] const int ntab = EPI == EPI_ROPE ? g.rope.npos * g.rope.half : 0;  // <= ROPE_TAB_MAX (host)
   if constexpr (EPI == EPI_ROPE) {
 #pragma unroll
     for (int i = 0; i < RTR; ++i) {
-      const int e = threadIdx.x + 512 * i;
+      const int e = threadIdx.x + NT * i;
       rpf[i] = e < ntab ? f32x2{g.rope.cos_t[e], g.rope.sin_t[e]} : f32x2{0.f, 0.f};
     }
   }
@@ -271,7 +285,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
   if constexpr (EPI == EPI_ROPE) {
 #pragma unroll
     for (int i = 0; i < RTR; ++i) {
-      const int e = threadIdx.x + 512 * i;
+      const int e = threadIdx.x + NT * i;
       if (e < ntab) rtab[e] = rpf[i];
     }
   }
@@ -285,12 +299,12 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
   auto rdA = [&](bf16x8 (&X)[4], int slot, int mh, int ks) {
     const LDS_AS char* s = smem + slot * STAGE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) X[i] = frag<AK, BM>(s, wr * 128 + (mh * 4 + i) * 16, ks, lane);
+    for (int i = 0; i < 4; ++i) X[i] = frag<AK, BM, BK>(s, wr * 128 + (mh * 4 + i) * 16, ks, lane);
   };
   auto rdB = [&](bf16x8 (&Y)[NTN], int slot, int ks) {
     const LDS_AS char* s = smem + slot * STAGE + A_BYTES;
 #pragma unroll
-    for (int j = 0; j < NTN; ++j) Y[j] = frag<BKM, BN>(s, wc * WN + j * 16, ks, lane);
+    for (int j = 0; j < NTN; ++j) Y[j] = frag<BKM, BN, BK>(s, wc * WN + j * 16, ks, lane);
   };
   // ---- fp8 (F8): one K-tile row is 128 B = 128 e4m3 values = ONE v_mfma_scale_f32_16x16x128_f8f6f4
   // per 16x16 output tile. Its 32-B lane operand is the two 16-B fragments the bf16 path reads for
@@ -427,6 +441,13 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
         __builtin_amdgcn_sched_barrier(0);
         mm8(Xa, 2, 0, NTN);
         __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (BK == 32) {
+        // one k-step: phase 0 = (M-half 0) under the read of M-half 1's A fragments; phase 1 after
+        // the barrier, the next K-tile's fragments read under its MFMAs
+        rdA(Ab, sl, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(Aa, 0, Ba);
+        __builtin_amdgcn_sched_barrier(0);
       } else {
       release(Aa, Ba);
       rdA(Ab, sl, 1, 0);
@@ -477,6 +498,14 @@ __global__ __launch_bounds__(512, 2) void k_gemm256(G256 g) {
         if (t + 1 < nk) rdB8(0, NTN / 2, sl ^ 1);
         __builtin_amdgcn_sched_barrier(0);
         mm8(Xb, 3, NTN / 2, NTN);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (BK == 32) {
+        mm(Ab, 1, Ba);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 1 < nk) {  // overwrite Aa / Ba once phase 1's MFMAs have been issued
+          rdA(Aa, sl ^ 1, 0, 0);
+          rdB(Ba, sl ^ 1, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
       } else {
       if (t + 1 < nk) {
@@ -876,8 +905,8 @@ int force_bn256() {
   return (e && e[0] == '1') ? 1 : 0;
 }
 
-int grid256(long nb) {
-  int per_xcd = num_cus() / 8;
+int grid256(long nb, int per_cu = 1) {
+  int per_xcd = per_cu * num_cus() / 8;
   const char* e = getenv("VJ_GEMM_PXCD");
   if (e && atoi(e) > 0) per_xcd = atoi(e);
   if (per_xcd < 1) per_xcd = 1;
@@ -912,6 +941,38 @@ int launch256_f8(int epi, const G256& g, hipStream_t st) {
     default: vj_set_error("vj_gemm_fp8: unsupported epilogue %d", epi); return VJ_ERR_ARG;
   }
   VJ_LAUNCH_CHECK("vj_gemm_fp8");
+  return VJ_OK;
+}
+
+// Two-workgroups-per-CU kernel (NWV = 4, 256 x 128 tiles, 32-deep K) for K-major GEMMs whose N
+// needs 128-wide tiles: its direct-store epilogue overlaps the other workgroup's MFMAs. Measured
+// (tools/bench_kernels.py): predictor fc2 N = 384 (f32 residual epilogue) -14 %, N = 384 bf16 even;
+// on 256-wide shapes its 32-deep main loop loses 10-20 %, so they stay on the 8-wave kernel.
+// VJ_GEMM_2W: 0 = never, 1 = every K-major GEMM, unset = the 128-wide shapes.
+int use_2w(bool narrow) {
+  const char* e = getenv("VJ_GEMM_2W");
+  if (e && e[0] == '0') return 0;
+  if (e && e[0] == '1') return 1;
+  return narrow ? 1 : 0;
+}
+
+int launch2w(int epi, G256 g, hipStream_t st) {
+  const dim3 grid(grid256((long)g.tiles_m * g.tiles_n, 2));
+  g.stagger = stagger_units(g.kslice);
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL((k_gemm256<true, true, EPI_BF16, 128, false, 4>), grid, dim3(256), 0, st, g); break;
+    case EPI_F32: hipLaunchKernelGGL((k_gemm256<true, true, EPI_F32, 128, false, 4>), grid, dim3(256), 0, st, g); break;
+    case EPI_F32_RESID:
+      hipLaunchKernelGGL((k_gemm256<true, true, EPI_F32_RESID, 128, false, 4>), grid, dim3(256), 0, st, g);
+      break;
+    case EPI_GELU: hipLaunchKernelGGL((k_gemm256<true, true, EPI_GELU, 128, false, 4>), grid, dim3(256), 0, st, g); break;
+    case EPI_GELU_BWD:
+      hipLaunchKernelGGL((k_gemm256<true, true, EPI_GELU_BWD, 128, false, 4>), grid, dim3(256), 0, st, g);
+      break;
+    case EPI_ROPE: hipLaunchKernelGGL((k_gemm256<true, true, EPI_ROPE, 128, false, 4>), grid, dim3(256), 0, st, g); break;
+    default: vj_set_error("gemm2w: bad epilogue %d", epi); return VJ_ERR_ARG;
+  }
+  VJ_LAUNCH_CHECK("vj_gemm256(2w)");
   return VJ_OK;
 }
 
@@ -961,6 +1022,10 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
     g.rope = *(const RopeP*)rope;
     if (g.rope.hd % 4 || g.rope.D % 4 || g.rope.npos < 1 || g.rope.npos > 1024) return VJ_ERR_UNSUPPORTED;
     if ((long)g.rope.npos * g.rope.half > ROPE_TAB_MAX) return VJ_ERR_UNSUPPORTED;
+  }
+  if (a_kmajor && b_kmajor && use_2w(bn == 128)) {
+    g.tiles_n = vj_cdiv(N, 128);
+    return launch2w(epi, g, st);
   }
   if (bn == 256) {
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);

@@ -434,8 +434,12 @@ __global__ void k_attn_delta(AttnArgs a) {
 // dK/dV: block = 4 waves x (32 KW) keys; sweep query tiles of 32 (Q, dO, lse, delta staged in LDS).
 // Each wave owns KW 32-key tiles (key tile kw of wave w: keys kw*128 + w*32 + 0..31 of the block),
 // so every staged Q / dO fragment feeds KW independent MFMA chains per barrier.
+// dK/dV workgroups per CU the register budget is sized for (head dims <= 64); 1 = no bound
+#ifndef VJ_ATTN_DKDV_OCC
+#define VJ_ATTN_DKDV_OCC 1
+#endif
 template <int HD, int KW>
-__global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
+__global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn_bwd_dkdv(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr int QT = 32;
   constexpr int TB = QT * HDP * 2;
@@ -625,8 +629,11 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
 // dQ: block = 4 waves x (32 QW) queries; sweep key tiles of 64 (K, V staged in LDS). Each wave owns
 // QW 32-query tiles (tile qw of wave w: queries qw*128 + w*32 + 0..31 of the block), so every K / V
 // fragment read from LDS feeds QW independent MFMA chains.
+#ifndef VJ_ATTN_DQ_OCC
+#define VJ_ATTN_DQ_OCC 1
+#endif
 template <int HD, int QW>
-__global__ __launch_bounds__(256) void k_attn_bwd_dq(AttnArgs a) {
+__global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_bwd_dq(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr int KT = 64;
   constexpr int TB = KT * HDP * 2;

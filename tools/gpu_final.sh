@@ -1,0 +1,18 @@
+#!/bin/bash
+# End-of-round measurement: full GPU tests, bench, kernel-trace stats, PMC passes (MFMA busy, HBM
+# fetch / write) and the dominant kernel's traffic; every GPU step under its own limit, stop at the
+# first failure. usage: tools/gpu_final.sh <tag>
+cd "$(dirname "$0")/.." || exit 2
+export TMPDIR=/tmp
+tag=${1:-final}
+out=gpurun_out/$tag
+mkdir -p "$out"
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > "$out/pytest.log" 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 "$out/pytest.log"; [ $rc -ge 2 ] && exit $rc
+timeout -k 10 300 python -u bench.py > "$out/bench.log" 2>&1 || { echo "bench failed"; tail -5 "$out/bench.log"; exit 3; }
+tail -c 600 "$out/bench.log"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --kernel-events 0 > "$out/prof.log" 2>&1 || { echo "prof failed"; tail -5 "$out/prof.log"; exit 4; }
+echo "prof ok"
+bash tools/pmc_bench.sh "$tag" > "$out/pmc.log" 2>&1 || { echo "pmc failed"; tail -5 "$out/pmc.log"; exit 5; }
+echo "pmc ok"
+python3 tools/traffic.py gpurun_out/pmc_bench/$tag/p2 gpurun_out/pmc_bench/$tag/p3 "k_gemm<1,1,EPI_F32_RESID>" "$out/traffic.json"

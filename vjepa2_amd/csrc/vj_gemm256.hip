@@ -209,7 +209,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   const int run0 = xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q;
   const int runend = run0 + q + (xcd < rmd ? 1 : 0);
   if (run0 + jb >= runend) return;
-  if (g.stagger > 0 && (jb & 1))
+  // stagger: the 8-wave kernel delays odd blocks of an XCD; the two-workgroup kernel delays the
+  // second workgroup of each CU (blocks jb and jb + P/2 of an XCD share a CU), so the two
+  // workgroups' epilogues fall under each other's main loops
+  if (g.stagger > 0 && (NWV == 4 ? jb >= (P >> 1) : (jb & 1)))
     for (int i = 0; i < g.stagger; ++i) __builtin_amdgcn_s_sleep(32);
 
   auto make_tile = [&](int wg) {

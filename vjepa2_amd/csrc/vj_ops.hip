@@ -28,16 +28,14 @@ __device__ __forceinline__ int f8_row_exp(float amax) {
   return min(max(e, -120), 120);
 }
 
-template <bool XBF, bool YF32, int NV, bool YF8 = false>
-__global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __restrict__ x, long ldx,
-                                                const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                float eps, void* __restrict__ y, long ldy, float* __restrict__ mean,
-                                                float* __restrict__ rstd, int* __restrict__ yexp = nullptr) {
-  const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  float4 v[NV];
-  float s = 0.f;
+// LN_RPW rows per wave: gamma / beta are loaded once per wave and the next row's x is fetched while
+// the current row is reduced and written (one row per wave re-read the 8 KB of gamma / beta for
+// every 4-6 KB row of traffic)
+constexpr int LN_RPW = 4;
+
+template <bool XBF, int NV>
+__device__ __forceinline__ void ln_load_row(const void* __restrict__ x, long ldx, long row, int D, int lane,
+                                            float4 (&v)[NV]) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = (i * 64 + lane) * 4;
@@ -48,61 +46,92 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
       } else {
         v[i] = *(const float4*)((const float*)x + row * ldx + c);
       }
-      s += v[i].x + v[i].y + v[i].z + v[i].w;
     }
   }
-  const float mu = wave_sum(s) / D;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    if (c < D) {
-      const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
-      q += a * a + b * b + cc * cc + d * d;
-    }
-  }
-  const float rs = rsqrtf(wave_sum(q) / D + eps);
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    const int c = (i * 64 + lane) * 4;
-    if (c < D) {
-      float o[4] = {(v[i].x - mu) * rs, (v[i].y - mu) * rs, (v[i].z - mu) * rs, (v[i].w - mu) * rs};
-      if (gamma) {
-        const float4 g = *(const float4*)(gamma + c);
-        const float4 b = *(const float4*)(beta + c);
-        o[0] = o[0] * g.x + b.x; o[1] = o[1] * g.y + b.y; o[2] = o[2] * g.z + b.z; o[3] = o[3] * g.w + b.w;
-      }
-      if constexpr (YF8) {
-        v[i] = make_float4(o[0], o[1], o[2], o[3]);  // kept for the scaled fp8 pass below
-      } else if constexpr (YF32) {
-        *(float4*)((float*)y + row * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
-      } else {
-        *(uint2*)((bf16_t*)y + row * ldy + c) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
-      }
-    }
-  }
-  if constexpr (YF8) {  // per-row scaled e4m3: y8 = e4m3(y * 2^-e), e = the least exponent with amax * 2^-e <= 448
-    float am = 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-      if ((i * 64 + lane) * 4 < D)
-        am = fmaxf(am, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
-    am = wave_max(am);
-    const int e = f8_row_exp(am);
-    const float sc = ldexpf(1.f, -e);
-    const bool bad = !(am <= 3.0e38f);  // inf / NaN row: every byte NaN (e4m3fn has no infinity)
+}
+
+template <bool XBF, bool YF32, int NV, bool YF8 = false>
+__global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __restrict__ x, long ldx,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                float eps, void* __restrict__ y, long ldy, float* __restrict__ mean,
+                                                float* __restrict__ rstd, int* __restrict__ yexp = nullptr) {
+  const int lane = threadIdx.x & 63;
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * LN_RPW;
+  if (row0 >= M) return;
+  float4 g[NV], bb[NV], v[NV], vn[NV];
+  if (gamma) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = (i * 64 + lane) * 4;
-      if (c < D)
-        *(uint32_t*)((unsigned char*)y + row * ldy + c) =
-            bad ? 0x7f7f7f7fu : f8pack4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
+      if (c < D) {
+        g[i] = *(const float4*)(gamma + c);
+        bb[i] = *(const float4*)(beta + c);
+      }
     }
-    if (lane == 0) yexp[row] = e;
   }
-  if (lane == 0) {
-    if (mean) mean[row] = mu;
-    if (rstd) rstd[row] = rs;
+  ln_load_row<XBF, NV>(x, ldx, row0, D, lane, v);
+#pragma unroll 1
+  for (int rr = 0; rr < LN_RPW; ++rr) {
+    const long row = row0 + rr;
+    if (row >= M) break;
+    if (rr + 1 < LN_RPW && row + 1 < M) ln_load_row<XBF, NV>(x, ldx, row + 1, D, lane, vn);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if ((i * 64 + lane) * 4 < D) s += v[i].x + v[i].y + v[i].z + v[i].w;
+    const float mu = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if ((i * 64 + lane) * 4 < D) {
+        const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
+        q += a * a + b * b + cc * cc + d * d;
+      }
+    }
+    const float rs = rsqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = (i * 64 + lane) * 4;
+      if (c < D) {
+        float o[4] = {(v[i].x - mu) * rs, (v[i].y - mu) * rs, (v[i].z - mu) * rs, (v[i].w - mu) * rs};
+        if (gamma) {
+          o[0] = o[0] * g[i].x + bb[i].x; o[1] = o[1] * g[i].y + bb[i].y;
+          o[2] = o[2] * g[i].z + bb[i].z; o[3] = o[3] * g[i].w + bb[i].w;
+        }
+        if constexpr (YF8) {
+          v[i] = make_float4(o[0], o[1], o[2], o[3]);  // kept for the scaled fp8 pass below
+        } else if constexpr (YF32) {
+          *(float4*)((float*)y + row * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+          *(uint2*)((bf16_t*)y + row * ldy + c) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+        }
+      }
+    }
+    if constexpr (YF8) {  // per-row scaled e4m3: y8 = e4m3(y * 2^-e), e = the least exponent with amax * 2^-e <= 448
+      float am = 0.f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        if ((i * 64 + lane) * 4 < D)
+          am = fmaxf(am, fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w))));
+      am = wave_max(am);
+      const int e = f8_row_exp(am);
+      const float sc = ldexpf(1.f, -e);
+      const bool bad = !(am <= 3.0e38f);  // inf / NaN row: every byte NaN (e4m3fn has no infinity)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const int c = (i * 64 + lane) * 4;
+        if (c < D)
+          *(uint32_t*)((unsigned char*)y + row * ldy + c) =
+              bad ? 0x7f7f7f7fu : f8pack4(v[i].x * sc, v[i].y * sc, v[i].z * sc, v[i].w * sc);
+      }
+      if (lane == 0) yexp[row] = e;
+    }
+    if (lane == 0) {
+      if (mean) mean[row] = mu;
+      if (rstd) rstd[row] = rs;
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = vn[i];
   }
 }
 
@@ -781,7 +810,7 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
   VJ_CHECK_ARG(D % 4 == 0 && D <= 64 * 4 * LN_MAXV, "vj_layernorm_fwd: D=%d must be %%4 and <= 2048", D);
   VJ_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "vj_layernorm_fwd: gamma/beta both or neither");
   VJ_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "vj_layernorm_fwd: strides must be %%4");
-  dim3 grid((M + 3) / 4);
+  dim3 grid((M + 4 * LN_RPW - 1) / (4 * LN_RPW));
   hipStream_t st = (hipStream_t)stream;
   const int nv = ln_nv(D);
 #define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, YF, NVV>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
@@ -1069,7 +1098,7 @@ extern "C" int vj_layernorm_fwd_fp8(int M, int D, const void* x, int x_bf16, lon
   VJ_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "vj_layernorm_fwd_fp8: gamma/beta both or neither");
   VJ_CHECK_ARG(ldx % 4 == 0 && ldy % 16 == 0 && !((uintptr_t)y8 & 15) && yexp,
                "vj_layernorm_fwd_fp8: fp8 rows must be 16-B aligned, exponents required");
-  dim3 grid((M + 3) / 4);
+  dim3 grid((M + 4 * LN_RPW - 1) / (4 * LN_RPW));
   hipStream_t st = (hipStream_t)stream;
 #define LNF8(XB, NVV)                                                                                             \
   hipLaunchKernelGGL((k_ln_fwd<XB, false, NVV, true>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y8, \

@@ -201,8 +201,9 @@ int vj_video_transform(int B, int T, int H, int W, int C, int S, const void* fra
 int vj_xattn_ws_floats(int B, int nq, int N, int H, int hd, long* out);
 int vj_xattn_fwd(int B, int nq, int N, int H, int hd, const void* q, long ldq, const void* kv, long ldkv, void* o,
                  long ldo, float* lse2, float scale, float* ws, long ws_floats, void* stream);
-/* SDPA backward of vj_xattn_fwd (nq <= 16): dq bf16 [B*nq][lddq], dkv bf16 [B*N][lddkv] (dk | dv, same
- * layout as kv, every element written). Deterministic: dq's cross-chunk sum is fixed-order. */
+/* SDPA backward of vj_xattn_fwd: dq bf16 [B*nq][lddq], dkv bf16 [B*N][lddkv] (dk | dv, same layout as
+ * kv, every element written). Deterministic: dq's cross-chunk sum and, for nq > 16, the dk / dv sum over
+ * query blocks (f32, in the workspace vj_xattn_ws_floats sizes) are fixed-order. */
 int vj_xattn_bwd(int B, int nq, int N, int H, int hd, const void* q, long ldq, const void* kv, long ldkv,
                  const void* o, long ldo, const void* dout, long lddo, const float* lse2, float scale, void* dq,
                  long lddq, void* dkv, long lddkv, float* ws, long ws_floats, void* stream);

@@ -53,7 +53,7 @@ def test_xattn_fwd_vs_fp32(B, nq, N, H, hd):
 
 
 @pytest.mark.parametrize("B,nq,N,H,hd", [(3, 1, 2048, 16, 64), (2, 3, 1000, 16, 88), (2, 16, 77, 12, 32),
-                                         (2, 3, 4600, 16, 80)])
+                                         (2, 3, 4600, 16, 80), (2, 37, 300, 4, 64)])
 def test_xattn_bwd_vs_fp32(B, nq, N, H, hd):
     from vjepa2_amd import ops
 

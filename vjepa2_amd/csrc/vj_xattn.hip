@@ -11,7 +11,8 @@
 // of a row); scores are computed key-per-thread (the 2 thread halves split the queries), the softmax
 // statistics per query by one wave, P.V by (key-group, column) threads. Partials (m, l, unnormalised O)
 // go to a workspace; a combine kernel merges the chunks in fixed order (deterministic, no atomics).
-// Queries are processed XQ = 16 at a time (the host walks larger nq in blocks).
+// Queries are processed XQ = 16 at a time (the host walks larger nq in blocks; the backward then
+// accumulates dK / dV over the blocks in an f32 workspace).
 //
 // Backward (SDPA's, for training the probe): per chunk, p = 2^(s2 - lse2), dp = dO.v, ds = p (dp - Dq)
 // with Dq = rowsum(dO * O); dK / dV rows of the chunk are complete (sums over the few queries) and
@@ -44,6 +45,10 @@ struct XArgs {
   long lddq;
   bf16_t* dkv;
   long lddkv;
+  // backward over more than XQ queries: dK / dV sum over every query block, accumulated in f32 rows
+  // laid out like dkv (first block writes, middle blocks add, the last block writes bf16 dkv)
+  float* dkv_acc;
+  int blk_first, blk_last;
 };
 
 // K / V rows of a chunk -> LDS [XCH][hd + 8] bf16 (row pad of 16 B: the per-key 16-B reads of the
@@ -235,6 +240,7 @@ __global__ __launch_bounds__(XNT) void k_xattn_bwd_part(XArgs a) {
       const float(*P)[XCH] = isv ? pp : dss;
       const float f = isv ? 1.f : a.scale;
       bf16_t* dst = a.dkv + (long)(b * a.N + k0 + j) * a.lddkv + (isv ? a.D : 0) + h * hd;
+      float* acc = a.dkv_acc ? a.dkv_acc + (long)(b * a.N + k0 + j) * (2L * a.D) + (isv ? a.D : 0) + h * hd : nullptr;
       for (int d = 0; d < hd; d += 8) {
         float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         for (int qi = 0; qi < nq; ++qi) {
@@ -242,8 +248,19 @@ __global__ __launch_bounds__(XNT) void k_xattn_bwd_part(XArgs a) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) s[e] = fmaf(pq, X[qi][d + e], s[e]);
         }
-        *(uint4*)(dst + d) = make_uint4(pack_bf2(f * s[0], f * s[1]), pack_bf2(f * s[2], f * s[3]),
-                                        pack_bf2(f * s[4], f * s[5]), pack_bf2(f * s[6], f * s[7]));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] *= f;
+        if (acc && !a.blk_first) {  // add the earlier query blocks' sums (fixed order: deterministic)
+          const float4 u = *(const float4*)(acc + d), w = *(const float4*)(acc + d + 4);
+          s[0] += u.x; s[1] += u.y; s[2] += u.z; s[3] += u.w; s[4] += w.x; s[5] += w.y; s[6] += w.z; s[7] += w.w;
+        }
+        if (acc && !a.blk_last) {
+          *(float4*)(acc + d) = make_float4(s[0], s[1], s[2], s[3]);
+          *(float4*)(acc + d + 4) = make_float4(s[4], s[5], s[6], s[7]);
+        } else {
+          *(uint4*)(dst + d) = make_uint4(pack_bf2(s[0], s[1]), pack_bf2(s[2], s[3]), pack_bf2(s[4], s[5]),
+                                          pack_bf2(s[6], s[7]));
+        }
       }
     }
   }
@@ -306,10 +323,12 @@ int check(const char* who, int B, int nq, int N, int H, int hd, long ldq, long l
 }  // namespace
 
 static long ws_floats_needed(int B, int N, int H, int hd) { return (long)B * H * vj_cdiv(N, XCH) * XQ * (hd + 2); }
+// backward with more than XQ queries: + the f32 dK / dV accumulator [B * N][2 * H * hd]
+static long bwd_acc_floats(int B, int nq, int N, int H, int hd) { return nq > XQ ? 2L * B * N * H * hd : 0; }
 
 extern "C" int vj_xattn_ws_floats(int B, int nq, int N, int H, int hd, long* out) {
   VJ_CHECK_ARG(out, "vj_xattn_ws_floats: null output");
-  *out = ws_floats_needed(B, N, H, hd);
+  *out = ws_floats_needed(B, N, H, hd) + bwd_acc_floats(B, nq, N, H, hd);
   return VJ_OK;
 }
 
@@ -343,9 +362,8 @@ extern "C" int vj_xattn_bwd(int B, int nq, int N, int H, int hd, const void* q, 
   VJ_CHECK_ARG(o && dout && lse2 && dq && dkv && ws, "vj_xattn_bwd: null argument");
   VJ_CHECK_ARG(lddkv >= 2L * H * hd && lddkv % 8 == 0 && ((uintptr_t)dkv & 15) == 0,
                "vj_xattn_bwd: dkv must be 16-B aligned with lddkv %% 8 == 0 (lddkv=%ld)", lddkv);
-  VJ_CHECK_ARG(ws_floats >= ws_floats_needed(B, N, H, hd), "vj_xattn_bwd: workspace needs %ld floats",
-               ws_floats_needed(B, N, H, hd));
-  VJ_CHECK_ARG(nq <= XQ, "vj_xattn_bwd: at most %d queries (got %d): dK / dV sum over all queries per chunk", XQ, nq);
+  const long need = ws_floats_needed(B, N, H, hd) + bwd_acc_floats(B, nq, N, H, hd);
+  VJ_CHECK_ARG(ws_floats >= need, "vj_xattn_bwd: workspace needs %ld floats", need);
   hipStream_t st = (hipStream_t)stream;
   XArgs a{};
   a.q = (const bf16_t*)q; a.ldq = ldq; a.kv = (const bf16_t*)kv; a.ldkv = ldkv;
@@ -353,8 +371,15 @@ extern "C" int vj_xattn_bwd(int B, int nq, int N, int H, int hd, const void* q, 
   a.nchunk = vj_cdiv(N, XCH); a.ws = ws; a.o = (bf16_t*)o; a.ldo = ldo; a.lse2 = (float*)lse2;
   a.dout = (const bf16_t*)dout; a.lddo = lddo; a.dq = (bf16_t*)dq; a.lddq = lddq; a.dkv = (bf16_t*)dkv;
   a.lddkv = lddkv;
-  hipLaunchKernelGGL(k_xattn_bwd_part, dim3(a.nchunk, B * H), dim3(XNT), kv_lds_bytes(hd), st, a);
-  hipLaunchKernelGGL(k_xattn_bwd_combine, dim3(B * H), dim3(XNT), 0, st, a);
+  a.dkv_acc = nq > XQ ? ws + ws_floats_needed(B, N, H, hd) : nullptr;
+  for (int q0 = 0; q0 < nq; q0 += XQ) {  // query blocks of XQ, in order (dq partials reuse the workspace)
+    a.q0 = q0;
+    a.nq = nq - q0 < XQ ? nq - q0 : XQ;
+    a.blk_first = q0 == 0;
+    a.blk_last = q0 + XQ >= nq;
+    hipLaunchKernelGGL(k_xattn_bwd_part, dim3(a.nchunk, B * H), dim3(XNT), kv_lds_bytes(hd), st, a);
+    hipLaunchKernelGGL(k_xattn_bwd_combine, dim3(B * H), dim3(XNT), 0, st, a);
+  }
   VJ_LAUNCH_CHECK("vj_xattn_bwd");
   return VJ_OK;
 }

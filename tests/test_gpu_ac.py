@@ -38,7 +38,8 @@ def _ref_attn(qkv, H, hd, groups, fblk):
 
 @pytest.mark.parametrize("hd,H,groups,fblk", [(64, 16, [(2, 1032)], 258), (64, 16, [(1, 2064)], 258),
                                               (32, 4, [(3, 18), (2, 30)], 6), (64, 2, [(2, 300)], 100),
-                                              (88, 2, [(1, 777)], 259), (32, 3, [(2, 129)], 43)])
+                                              (88, 2, [(1, 777)], 259), (32, 3, [(2, 129)], 43),
+                                              (64, 2, [(1, 500), (2, 70)], 130)])  # partial last frame
 def test_frame_causal_attention_vs_fp32(hd, H, groups, fblk):
     from vjepa2_amd import ops
 
@@ -122,3 +123,27 @@ def test_ac_predictor_256px_vs_oracle():
             continue
         e = rel_l1(p.grad, sd[n].grad)
         assert e < 4e-2, (n, e)
+
+
+def test_acblock_standalone_forward():
+    """ACBlock.forward / ACRoPEAttention.forward called directly with the reference's arguments
+    (modules.py:488-497: attn_mask from build_action_block_causal_attention_mask, T, H, W,
+    action_tokens) against the oracle's ac_block; any other attn_mask is refused."""
+    import torch.nn as nn
+
+    from oracle import vjepa_oracle as orc
+    from vjepa2_amd.modules import ACBlock, build_action_block_causal_attention_mask
+
+    torch.manual_seed(3)
+    T, H, W, A, D = 3, 4, 4, 2, 128
+    blk = ACBlock(dim=D, num_heads=2, mlp_ratio=4.0, qkv_bias=True, use_rope=True, grid_size=H,
+                  norm_layer=lambda d: nn.LayerNorm(d, eps=1e-6))
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+    x = torch.randn(2, T * (A + H * W), D)
+    mask = build_action_block_causal_attention_mask(T, H, W, A)
+    with torch.no_grad():
+        ref = orc.ac_block(x, sd, "", 2, T, H, W, A, mask, H)
+        got = blk.to(DEV)(x.to(DEV), attn_mask=mask.to(DEV), T=T, H=H, W=W, action_tokens=A)
+    assert rel_l1(got, ref) < 1e-2, rel_l1(got, ref)
+    with pytest.raises(NotImplementedError):
+        blk(x.to(DEV), attn_mask=torch.ones_like(mask).to(DEV), T=T, H=H, W=W, action_tokens=A)

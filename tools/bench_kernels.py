@@ -132,6 +132,35 @@ def attn_case(lib, hd, H, groups, dev, stream, bwd):
     return (bwdf, 2.5 * fl) if bwd else (fwd, fl)  # backward: FA2 convention, 5 matmuls
 
 
+# (name, M, D, with dres_in): LayerNorm backward of the block's norm1 / norm2 (dres out f32 + bf16
+# copy, dgamma / dbeta partials); the "TF" column is TB/s of algorithmic bytes for these
+LNB = [("ln bwd ctx", 11712, 1024, True), ("ln bwd tgt-size", 49152, 1024, True), ("ln bwd pred", 71232, 384, True)]
+
+
+def ln_bwd_case(lib, M, D, acc, dev, stream):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(M, D, generator=g).to(dev)
+    dy = torch.randn(M, D, generator=g).to(dev).bfloat16()
+    mean = x.mean(1).contiguous()
+    rstd = (x.var(1, unbiased=False) + 1e-6).rsqrt().contiguous()
+    gamma = torch.rand(D, generator=g).to(dev)
+    dres_in = torch.randn(M, D, generator=g).to(dev) if acc else None
+    dres = torch.empty(M, D, device=dev)
+    dres_bf = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    dgamma = torch.empty(D, device=dev)
+    dbeta = torch.empty(D, device=dev)
+    nb = lib.vj_layernorm_bwd_blocks(M)
+    ws = torch.empty(nb * 2 * D, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+
+    def run():
+        rc = lib.vj_layernorm_bwd(M, D, p(dy), D, p(x), D, p(mean), p(rstd), p(gamma), p(dres_in), D, p(dres), D,
+                                  p(dres_bf), D, p(dgamma), p(dbeta), None, None, p(ws), ws.numel(), stream)
+        assert rc == 0, rc
+    byt = M * D * (4 + 2 + 4 + 2 + (4 if acc else 0))
+    return run, byt * 1e3
+
+
 def time_fn(fn, iters=10):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
@@ -181,6 +210,10 @@ def main():
         if only and only not in name:
             continue
         cases.append((name, [attn_case(lib, hd, H, groups, dev, stream, bwd) for lib in libs]))
+    for name, M, D, acc in LNB:
+        if only and only not in name:
+            continue
+        cases.append((name, [ln_bwd_case(lib, M, D, acc, dev, stream) for lib in libs]))
     names = [os.path.basename(p).replace("libvjepa_hip", "lib")[:14] + ("@" + ",".join(f"{k[7:] if k.startswith('VJ_GEMM_') else k}={v}" for k, v in e.items()) if e else "") for p, e in cols]
     print(f"{'case':22s} " + " ".join(f"{n[:26]:>26s}" for n in names), flush=True)
     for name, runs in cases:

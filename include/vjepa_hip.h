@@ -152,9 +152,11 @@ int vj_pred_index(int B, int K, int Kp, const long* mx, const long* my, int row0
 int vj_ids64to32(long n, const long* in, int* out, void* stream);
 
 /* Fused forward_target normalisation + JEPA loss + dL/dz (train.py:414-435). */
-/* z: predictor output rows (bf16 if z_bf16 else f32); rows split into ngroups mask groups of
- * group_rows[g] rows; per-row weight pair_weight / (group_rows[g] * D). dz is bf16. */
-int vj_jepa_loss(int R, int D, const void* z, int z_bf16, long ldz, const float* tgt, long ldt, const int* loss_rows,
+/* z: predictor output rows (bf16 if z_bf16 else f32); tgt: target-encoder rows (bf16 if tgt_bf16
+ * else f32); rows split into ngroups mask groups of group_rows[g] rows; per-row weight
+ * pair_weight / (group_rows[g] * D). dz is bf16. */
+int vj_jepa_loss(int R, int D, const void* z, int z_bf16, long ldz, const void* tgt, int tgt_bf16, long ldt,
+                 const int* loss_rows,
                  const float* gamma, const float* beta, float eps1, float eps2, float loss_exp, int ngroups,
                  const int* group_rows, float pair_weight, void* dz, long lddz, float* row_loss, float* loss_out,
                  void* stream);

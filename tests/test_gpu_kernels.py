@@ -104,6 +104,10 @@ def test_gemm_epilogues(M, N):
     resid = torch.randn(M, N, generator=g).to(DEV)
     y = ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid)
     _close(y, ref + resid, 2e-4, 1e-5, "EPI_F32_RESID")
+    rb = resid.bfloat16()  # bf16 residual stream (no-grad target encoder): one rounding of acc + b + r
+    y = ops.linear_fwd(X, W, b, ops.EPI_BF16_RESID, resid=rb)
+    assert y.dtype == torch.bfloat16
+    _close(y, ref + rb.float(), 1e-3, 8e-3, "EPI_BF16_RESID")
     pre = ops.linear_fwd(X, W, b, ops.EPI_BF16)  # the same bf16 pre-activation the GELU epilogue rounds
     dgelu, act = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
     _, act2 = ops.linear_fwd(X, W, b, ops.EPI_GELU)  # no derivative requested (no-grad target path)

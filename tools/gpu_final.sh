@@ -15,4 +15,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --outpu
 echo "prof ok"
 bash tools/pmc_bench.sh "$tag" > "$out/pmc.log" 2>&1 || { echo "pmc failed"; tail -5 "$out/pmc.log"; exit 5; }
 echo "pmc ok"
-python3 tools/traffic.py gpurun_out/pmc_bench/$tag/p2 gpurun_out/pmc_bench/$tag/p3 "k_gemm<1,1,EPI_F32_RESID>" "$out/traffic.json"
+# the bench's own dominant kernel (roofline.kernel of its JSON line)
+dom=$(python3 -c "import json,sys; print(json.loads([l for l in open('$out/bench.log') if l.startswith('{')][-1])['roofline']['kernel'])")
+echo "dominant: $dom"
+python3 tools/traffic.py gpurun_out/pmc_bench/$tag/p2 gpurun_out/pmc_bench/$tag/p3 "$dom" "$out/traffic.json"

@@ -17,7 +17,7 @@ import re
 import sys
 
 EPI = {"EPI_BF16": 0, "EPI_F32": 1, "EPI_F32_RESID": 2, "EPI_GELU": 3, "EPI_GELU_BWD": 4, "EPI_ROPE": 5,
-       "EPI_PARTIAL": 6}
+       "EPI_PARTIAL": 6, "EPI_BF16_RESID": 7}
 
 
 def name_regex(label):

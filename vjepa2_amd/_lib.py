@@ -54,7 +54,7 @@ SIGNATURES = {
     "vj_add_rows": [_I, _I, _P, _L, _P, _L, _P, _I, _P],
     "vj_pred_index": [_I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P],
     "vj_ids64to32": [_L, _P, _P, _P],
-    "vj_jepa_loss": [_I, _I, _P, _I, _L, _P, _L, _P, _P, _P, _F, _F, _F, _I, _P, _F, _P, _L, _P, _P, _P],
+    "vj_jepa_loss": [_I, _I, _P, _I, _L, _P, _I, _L, _P, _P, _P, _F, _F, _F, _I, _P, _F, _P, _L, _P, _P, _P],
     "vj_check_finite": [_L, _P, _P, _P],
     "vj_adamw": [_L, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, _P, _P],
     "vj_ema": [_L, _P, _P, _F, _P, _P],

@@ -23,7 +23,7 @@
 
 namespace {
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_PARTIAL = 5 };
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_PARTIAL = 5, EPI_BF16_RESID = 7 };
 
 struct GemmArgs {
   const bf16_t* A;
@@ -178,6 +178,9 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         } else if constexpr (EPI == EPI_F32_RESID) {
           const float res = ((const float*)g.aux)[(long)m * g.ldaux + n];
           ((float*)g.C)[(long)m * g.ldc + n] = res + v;
+        } else if constexpr (EPI == EPI_BF16_RESID) {
+          const float res = bf2f(((const bf16_t*)g.aux)[(long)m * g.ldaux + n]);
+          ((bf16_t*)g.C)[(long)m * g.ldc + n] = f2bf(res + v);
         } else if constexpr (EPI == EPI_GELU) {
           float y, dy;
           gelu_fwd_grad(bf2f(f2bf(v)), y, dy);  // on the bf16 pre-activation
@@ -239,6 +242,7 @@ int launch_epi(int epi, const GemmArgs& g, dim3 grid, hipStream_t st) {
     case EPI_F32_RESID: hipLaunchKernelGGL((k_gemm<AK, BKM, EPI_F32_RESID>), grid, dim3(256), 0, st, g); break;
     case EPI_GELU: hipLaunchKernelGGL((k_gemm<AK, BKM, EPI_GELU>), grid, dim3(256), 0, st, g); break;
     case EPI_GELU_BWD: hipLaunchKernelGGL((k_gemm<AK, BKM, EPI_GELU_BWD>), grid, dim3(256), 0, st, g); break;
+    case EPI_BF16_RESID: hipLaunchKernelGGL((k_gemm<AK, BKM, EPI_BF16_RESID>), grid, dim3(256), 0, st, g); break;
     default: vj_set_error("vj_gemm_bf16: unknown epilogue %d", epi); return VJ_ERR_ARG;
   }
   VJ_LAUNCH_CHECK("vj_gemm_bf16");
@@ -277,7 +281,8 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
   VJ_CHECK_ARG(a_kmajor ? lda >= K : lda >= M, "vj_gemm_bf16: lda too small");
   VJ_CHECK_ARG(b_kmajor ? ldb >= K : ldb >= N, "vj_gemm_bf16: ldb too small");
   VJ_CHECK_ARG(epi == EPI_GELU ? (C2 != nullptr) : (C != nullptr), "vj_gemm_bf16: null output");
-  VJ_CHECK_ARG((epi != EPI_F32_RESID && epi != EPI_GELU_BWD) || aux, "vj_gemm_bf16: epilogue needs aux");
+  VJ_CHECK_ARG((epi != EPI_F32_RESID && epi != EPI_GELU_BWD && epi != EPI_BF16_RESID) || aux,
+               "vj_gemm_bf16: epilogue needs aux");
   // 32-bit DMA offsets: every operand must span < 2 GB from its tile origin.
   VJ_CHECK_ARG((a_kmajor ? (long)M * lda : (long)K * lda) * 2 < 0x7fffffffL, "vj_gemm_bf16: A too large");
   VJ_CHECK_ARG((b_kmajor ? (long)N * ldb : (long)K * ldb) * 2 < 0x7fffffffL, "vj_gemm_bf16: B too large");

@@ -33,7 +33,10 @@
 
 namespace {
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5, EPI_PARTIAL = 6 };
+// EPI_BF16_RESID: bf16 residual in (aux), bf16 out — the no-grad target encoder's residual stream in
+// the reference's own autocast precision (x = x + proj(...) in bf16), half the epilogue bytes of F32_RESID
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5, EPI_PARTIAL = 6,
+       EPI_BF16_RESID = 7 };
 
 using RopeP = VjRope;
 
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // K-major B with 4 n-tiles per wave: permuted B staging + stores straight from registers (16-B
   // f32 / 8-B bf16 per row); 128-wide tiles would store 4-8 B per lane, so they keep the LDS path
   constexpr bool DIRECT = BKM && NTN == 4;
-  constexpr bool AUX = EPI == EPI_F32_RESID || EPI == EPI_GELU_BWD;
+  constexpr bool AUX = EPI == EPI_F32_RESID || EPI == EPI_GELU_BWD || EPI == EPI_BF16_RESID;
   constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_F32_RESID || EPI == EPI_PARTIAL;
 
   // The next tile's stage 0 is DMA'd during this tile's last K-tile. Its stage 1 goes out right
@@ -713,7 +716,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
               v[2 * p + 1] = x1 * b[0] + x0 * b[1];
             }
           }
-          if constexpr (EPI == EPI_F32_RESID) {
+          if constexpr (EPI == EPI_F32_RESID || EPI == EPI_BF16_RESID) {
 #pragma unroll
             for (int j = 0; j < NTN; ++j) v[j] += aux[i % (AUX_PF + 1)][r][j];
           }
@@ -797,7 +800,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         // residual / GELU pre-activation rows of this pass fetched up front: one memory latency per
         // pass instead of one per row
         [[maybe_unused]] float4 rres[EPI == EPI_F32_RESID ? IT : 1];
-        [[maybe_unused]] uint2 rpre[EPI == EPI_GELU_BWD ? IT : 1];
+        [[maybe_unused]] uint2 rpre[EPI == EPI_GELU_BWD || EPI == EPI_BF16_RESID ? IT : 1];
         if constexpr (AUX) {
 #pragma unroll
           for (int it = 0; it < IT; ++it) {
@@ -843,6 +846,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
             const uint32_t a0 = gelu_pair(pack_bf2(v[0], v[1]), &d0), a1 = gelu_pair(pack_bf2(v[2], v[3]), &d1);
             if (g.C) *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(d0, d1);
             *(uint2*)((bf16_t*)g.C2 + (long)m * g.ldc2 + n) = make_uint2(a0, a1);
+          } else if constexpr (EPI == EPI_BF16_RESID) {
+            const uint2 pu = rpre[it];  // bf16 residual
+            auto lo = [](uint32_t u) { return __builtin_bit_cast(float, u << 16); };
+            auto hi = [](uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); };
+            *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) =
+                make_uint2(pack_bf2(lo(pu.x) + v[0], hi(pu.x) + v[1]), pack_bf2(lo(pu.y) + v[2], hi(pu.y) + v[3]));
           } else {  // EPI_GELU_BWD
             const uint2 pu = rpre[it];  // saved GELU derivative (bf16)
             auto lo = [](uint32_t u) { return __builtin_bit_cast(float, u << 16); };
@@ -973,6 +982,9 @@ int launch2w(int epi, G256 g, hipStream_t st) {
       hipLaunchKernelGGL((k_gemm256<true, true, EPI_GELU_BWD, 128, false, 4>), grid, dim3(256), 0, st, g);
       break;
     case EPI_ROPE: hipLaunchKernelGGL((k_gemm256<true, true, EPI_ROPE, 128, false, 4>), grid, dim3(256), 0, st, g); break;
+    case EPI_BF16_RESID:
+      hipLaunchKernelGGL((k_gemm256<true, true, EPI_BF16_RESID, 128, false, 4>), grid, dim3(256), 0, st, g);
+      break;
     default: vj_set_error("gemm2w: bad epilogue %d", epi); return VJ_ERR_ARG;
   }
   VJ_LAUNCH_CHECK("vj_gemm256(2w)");
@@ -990,6 +1002,13 @@ int launch256(int epi, const G256& g, hipStream_t st) {
     case EPI_GELU: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_GELU, BN>), grid, dim3(512), 0, st, g); break;
     case EPI_GELU_BWD: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_GELU_BWD, BN>), grid, dim3(512), 0, st, g); break;
     case EPI_ROPE: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_ROPE, BN>), grid, dim3(512), 0, st, g); break;
+    case EPI_BF16_RESID:  // forward GEMMs only (A and B K-major); other layouts take the generic kernel
+      if constexpr (AK && BKM) {
+        hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_BF16_RESID, BN>), grid, dim3(512), 0, st, g);
+        break;
+      } else {
+        return VJ_ERR_UNSUPPORTED;
+      }
     case EPI_PARTIAL:  // split-K weight gradients only: dY^T X, both operands MN-major
       if constexpr (!AK && !BKM) {
         hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_PARTIAL, BN>), grid, dim3(512), 0, st, g);
@@ -1010,7 +1029,8 @@ int launch256(int epi, const G256& g, hipStream_t st) {
 int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
                         int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
                         void* C2, long ldc2, hipStream_t st, const void* rope) {
-  if (epi < EPI_BF16 || epi > EPI_ROPE || N % 8 || ldc % 4 || ldc2 % 4 || ldaux % 4) return VJ_ERR_UNSUPPORTED;
+  if (epi < EPI_BF16 || (epi > EPI_ROPE && epi != EPI_BF16_RESID) || N % 8 || ldc % 4 || ldc2 % 4 || ldaux % 4)
+    return VJ_ERR_UNSUPPORTED;
   if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
     return VJ_ERR_UNSUPPORTED;
   // 256-wide tiles (direct-store epilogue) unless the last column tile would waste > 15 % of the work

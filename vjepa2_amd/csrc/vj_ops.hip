@@ -580,9 +580,9 @@ struct LossGroups {
   int rows[4];
   float pair_weight;  // 1 / (number of (fpc, mask) pairs averaged by the loss)
 };
-template <bool ZBF>
+template <bool ZBF, bool TBF>
 __global__ __launch_bounds__(256) void k_jepa_loss(int R, int D, const void* __restrict__ zp, long ldz,
-                                                   const float* __restrict__ tgt, long ldt,
+                                                   const void* __restrict__ tgt, long ldt,
                                                    const int* __restrict__ loss_rows, const float* __restrict__ gamma,
                                                    const float* __restrict__ beta, float eps1, float eps2, float p,
                                                    LossGroups lg, bf16_t* __restrict__ dz, long lddz,
@@ -594,14 +594,19 @@ __global__ __launch_bounds__(256) void k_jepa_loss(int R, int D, const void* __r
   long acc = lg.rows[0];
   while (g < lg.ngroups - 1 && r >= acc) acc += lg.rows[++g];
   const float w = lg.pair_weight / ((float)lg.rows[g] * (float)D);
-  const float* t = tgt + (long)loss_rows[r] * ldt;
+  const long trow = (long)loss_rows[r] * ldt;
   float4 v[LN_MAXV];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < LN_MAXV; ++i) {
     const int c = (i * 64 + lane) * 4;
     if (c < D) {
-      v[i] = *(const float4*)(t + c);
+      if constexpr (TBF) {  // bf16 target rows (the target encoder's bf16 residual stream)
+        const uint2 u = *(const uint2*)((const bf16_t*)tgt + trow + c);
+        v[i] = make_float4(bf2f(u.x & 0xffff), bf2f(u.x >> 16), bf2f(u.y & 0xffff), bf2f(u.y >> 16));
+      } else {
+        v[i] = *(const float4*)((const float*)tgt + trow + c);
+      }
       s += v[i].x + v[i].y + v[i].z + v[i].w;
     }
   }
@@ -982,7 +987,7 @@ extern "C" int vj_ids64to32(long n, const long* in, int* out, void* stream) {
   return VJ_OK;
 }
 
-extern "C" int vj_jepa_loss(int R, int D, const void* z, int z_bf16, long ldz, const float* tgt, long ldt,
+extern "C" int vj_jepa_loss(int R, int D, const void* z, int z_bf16, long ldz, const void* tgt, int tgt_bf16, long ldt,
                             const int* loss_rows, const float* gamma, const float* beta, float eps1, float eps2,
                             float loss_exp, int ngroups, const int* group_rows, float pair_weight, void* dz, long lddz,
                             float* row_loss, float* loss_out, void* stream) {
@@ -999,12 +1004,14 @@ extern "C" int vj_jepa_loss(int R, int D, const void* z, int z_bf16, long ldz, c
   }
   VJ_CHECK_ARG(tot == R, "vj_jepa_loss: groups cover %ld rows, R=%d", tot, R);
   hipStream_t st = (hipStream_t)stream;
-  if (z_bf16)
-    hipLaunchKernelGGL(k_jepa_loss<true>, dim3((R + 3) / 4), dim3(256), 0, st, R, D, z, ldz, tgt, ldt, loss_rows, gamma,
-                       beta, eps1, eps2, loss_exp, lg, (bf16_t*)dz, lddz, row_loss);
-  else
-    hipLaunchKernelGGL(k_jepa_loss<false>, dim3((R + 3) / 4), dim3(256), 0, st, R, D, z, ldz, tgt, ldt, loss_rows, gamma,
-                       beta, eps1, eps2, loss_exp, lg, (bf16_t*)dz, lddz, row_loss);
+#define JL(ZB, TB)                                                                                                \
+  hipLaunchKernelGGL((k_jepa_loss<ZB, TB>), dim3((R + 3) / 4), dim3(256), 0, st, R, D, z, ldz, tgt, ldt, loss_rows, \
+                     gamma, beta, eps1, eps2, loss_exp, lg, (bf16_t*)dz, lddz, row_loss)
+  if (z_bf16 && tgt_bf16) JL(true, true);
+  else if (z_bf16) JL(true, false);
+  else if (tgt_bf16) JL(false, true);
+  else JL(false, false);
+#undef JL
   hipLaunchKernelGGL(k_sum1, dim3(1), dim3(256), 0, st, (long)R, row_loss, loss_out);
   VJ_LAUNCH_CHECK("vj_jepa_loss");
   return VJ_OK;

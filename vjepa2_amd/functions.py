@@ -13,7 +13,7 @@ autograd only carries activation gradients between layers.
 import torch
 
 from . import ops
-from .ops import BF16, EPI_BF16, EPI_F32, EPI_F32_RESID, EPI_GELU, F32
+from .ops import BF16, EPI_BF16, EPI_BF16_RESID, EPI_F32, EPI_F32_RESID, EPI_GELU, F32
 
 # ------------------------------------------------------------------------------------------------
 # parameter views
@@ -117,6 +117,12 @@ def _attn_scale(attn, hd):
     return hd**-0.5 if attn.use_sdpa else attn.scale
 
 
+def _resid_epi(x):
+    # bf16 residual stream only on the no-grad target encoder (VisionTransformer.forward_features with
+    # bf16_residual): the reference's own autocast precision, half the residual bytes
+    return EPI_BF16_RESID if x.dtype == BF16 else EPI_F32_RESID
+
+
 def block_forward_fp8(x, blk, lay):
     """Forward-only block with the QKV and fc1 GEMMs on the fp8 MFMA (opt-in for the no-grad target
     encoder, BASELINE configs[4]): LN1 / LN2 write per-row scaled e4m3, the weights are per-channel
@@ -133,15 +139,16 @@ def block_forward_fp8(x, blk, lay):
     else:
         qkv = ops.linear_fwd_fp8(ln1, e1, w8, ew, attn.qkv.bias, EPI_BF16)
     o, _ = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd), fblk=lay.fblk)
-    x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32_RESID, resid=x)
+    x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, _resid_epi(x), resid=x)
     ln2, e2 = ops.layernorm_fwd_fp8(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
     w18, ew1 = weight_fp8(mlp.fc1.weight)
     _, act = ops.linear_fwd_fp8(ln2, e2, w18, ew1, mlp.fc1.bias, EPI_GELU)
-    return ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_F32_RESID, resid=x_mid)
+    return ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, _resid_epi(x), resid=x_mid)
 
 
 def block_forward(x, blk, lay, save):
     T, D = x.shape
+    assert not (save and x.dtype == BF16), "the training path keeps the residual stream in f32"
     attn, mlp = blk.attn, blk.mlp
     H = attn.num_heads
     hd = D // H
@@ -153,13 +160,13 @@ def block_forward(x, blk, lay, save):
     else:
         qkv = ops.linear_fwd(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
     o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd), fblk=lay.fblk)
-    x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32_RESID, resid=x)
+    x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, _resid_epi(x), resid=x)
     ln2, m2, r2 = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, want_stats=save)
     hidden = mlp.fc1.weight.shape[0]
     # the fc1 epilogue saves GELU'(pre-activation) for the backward (bf16, the bytes the pre-activation took)
     dgelu = torch.empty(T, hidden, dtype=BF16, device=x.device) if save else None
     _, act = ops.linear_fwd(ln2, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=dgelu)
-    x_out = ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_F32_RESID, resid=x_mid)
+    x_out = ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, _resid_epi(x), resid=x_mid)
     saved = (x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, dgelu, act) if save else None
     return x_out, saved
 

@@ -9,7 +9,8 @@ import torch
 from ._lib import call, int_array
 
 EPI_BF16, EPI_F32, EPI_F32_RESID, EPI_GELU, EPI_GELU_BWD = 0, 1, 2, 3, 4
-EPI_NAMES = ["EPI_BF16", "EPI_F32", "EPI_F32_RESID", "EPI_GELU", "EPI_GELU_BWD"]
+EPI_BF16_RESID = 7  # bf16 residual in, bf16 out (no-grad target encoder: the reference's autocast precision)
+EPI_NAMES = ["EPI_BF16", "EPI_F32", "EPI_F32_RESID", "EPI_GELU", "EPI_GELU_BWD", "EPI_5", "EPI_6", "EPI_BF16_RESID"]
 BF16 = torch.bfloat16
 F32 = torch.float32
 
@@ -143,6 +144,9 @@ def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
             assert resid is not None and resid.dtype == F32 and resid.shape == (M, N)
     elif epi == EPI_GELU:
         out2 = out2 if out2 is not None else torch.empty(M, N, dtype=BF16, device=x.device)
+    elif epi == EPI_BF16_RESID:
+        assert resid is not None and resid.dtype == BF16 and resid.shape == (M, N)
+        out = out if out is not None else torch.empty(M, N, dtype=BF16, device=x.device)
     ldc = out.stride(0) if out is not None else 0
     ldc2 = out2.stride(0) if out2 is not None else 0
     gemm(M, N, K, x, lda, True, w, ldb, True, epi, out=out, ldc=ldc, out2=out2, ldc2=ldc2, bias=bias,
@@ -508,13 +512,13 @@ def jepa_loss(z, tgt, loss_rows, gamma, beta, group_rows, eps1=1e-6, eps2=1e-5, 
     """Returns (loss f32 [1], dz bf16 [R, D], row_loss f32 [R]). z bf16 or f32 [R, D]; the loss is the
     mean over `npairs` (default len(group_rows)) of each mask group's mean |z - h|^p / p."""
     _dev(z, tgt, loss_rows)
-    assert z.dtype in (F32, BF16)
+    assert z.dtype in (F32, BF16) and tgt.dtype in (F32, BF16)
     R, D = z.shape
     npairs = len(group_rows) if npairs is None else npairs
     dz = torch.empty(R, D, dtype=BF16, device=z.device)
     row_loss = torch.empty(R, dtype=F32, device=z.device)
     loss = torch.empty(1, dtype=F32, device=z.device)
-    _call("vj_jepa_loss", R, D, _p(z), int(z.dtype == BF16), _rowmajor(z, "z"), _p(tgt), _rowmajor(tgt, "tgt"),
+    _call("vj_jepa_loss", R, D, _p(z), int(z.dtype == BF16), _rowmajor(z, "z"), _p(tgt), int(tgt.dtype == BF16), _rowmajor(tgt, "tgt"),
          _p(loss_rows), _p(gamma), _p(beta), float(eps1), float(eps2), float(loss_exp), len(group_rows),
          int_array(group_rows), 1.0 / npairs, _p(dz), D, _p(row_loss), _p(loss), _stream())
     return loss, dz, row_loss

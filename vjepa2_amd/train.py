@@ -110,7 +110,7 @@ class JEPATrainer:
     """The fused V-JEPA train step (app/vjepa/train.py:409-471) over arena-owned parameters."""
 
     def __init__(self, encoder, predictor, target_encoder, optimizer, mixed_precision=True, loss_exp=1.0, world_size=1,
-                 bucket_mb=64, group=None, fp8_target=False):
+                 bucket_mb=64, group=None, fp8_target=False, target_bf16_residual=None):
         unwrap = lambda m: getattr(m, "backbone", getattr(m, "module", m))  # noqa: E731
         self.enc, self.pred, self.tgt = unwrap(encoder), unwrap(predictor), unwrap(target_encoder)
         self.opt = optimizer
@@ -119,6 +119,12 @@ class JEPATrainer:
         self.world = world_size
         # opt-in: the no-grad target encoder's QKV / fc1 GEMMs on the fp8 MFMA (functions.block_forward_fp8)
         self.fp8_target = fp8_target
+        # the no-grad target encoder's residual stream in bf16 (the reference's autocast precision;
+        # half the bytes of its proj / fc2 epilogues and LayerNorm reads). Default on; env
+        # VJ_TARGET_BF16=0 or target_bf16_residual=False keeps it f32.
+        if target_bf16_residual is None:
+            target_bf16_residual = os.environ.get("VJ_TARGET_BF16", "1") != "0"
+        self.target_bf16_residual = bool(target_bf16_residual)
         enc_w, pred_w, enc_n, pred_n = optimizer.arenas
         device = enc_w.data.device
         tnamed = dict(target_encoder.named_parameters())
@@ -153,10 +159,10 @@ class JEPATrainer:
             main = torch.cuda.current_stream()
             side.wait_stream(main)  # clips + this step's EMA'd target weights are ready
             with torch.cuda.stream(side), torch.no_grad():
-                h = self.tgt.forward_features(clips, fp8=self.fp8_target)
+                h = self.tgt.forward_features(clips, fp8=self.fp8_target, bf16_residual=self.target_bf16_residual)
         else:
             with torch.no_grad():
-                h = self.tgt.forward_features(clips, fp8=self.fp8_target)
+                h = self.tgt.forward_features(clips, fp8=self.fp8_target, bf16_residual=self.target_bf16_residual)
         z, _ = self.enc.forward_ragged(clips, masks_enc, out_dtype=torch.bfloat16)
         zp, pl = self.pred.forward_ragged(z, masks_enc, masks_pred, mask_index=mask_index, out_dtype=torch.bfloat16)
         if side is not None:

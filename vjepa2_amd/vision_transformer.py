@@ -154,10 +154,13 @@ class VisionTransformer(nn.Module):
         t = fn.run_patch_embed(x, self.patch_embed, masks, pos_table=pos, pos_ids=lay.ids, pos_mod=N)
         return t, lay
 
-    def forward_ragged(self, x, masks, out_dtype=torch.bfloat16, final_norm=True, fp8=False):
+    def forward_ragged(self, x, masks, out_dtype=torch.bfloat16, final_norm=True, fp8=False, bf16_residual=False):
         """All masks in ONE pass. Returns (tokens [sum_m B*K_m, D], layout). fp8: QKV / fc1 GEMMs on
-        the fp8 MFMA (forward-only, functions.block_forward_fp8)."""
+        the fp8 MFMA (forward-only, functions.block_forward_fp8). bf16_residual (no-grad only): the
+        residual stream in bf16, as the reference's autocast keeps it (x = x + proj(...) in bf16)."""
         t, lay = self.tokens(x, masks)
+        if bf16_residual:
+            t = ops.cast_bf16(t)
         for blk in self.blocks:
             t = fn.run_block(t, blk, lay, fp8=fp8)
         if final_norm:
@@ -165,10 +168,10 @@ class VisionTransformer(nn.Module):
         return t, lay
 
     @torch.no_grad()
-    def forward_features(self, x, fp8=False):
-        """All tokens, no final norm (f32 residual stream [B*N, D]); used by the target encoder,
-        whose final norm is fused into the JEPA loss kernel."""
-        t, _ = self.forward_ragged(x, None, final_norm=False, fp8=fp8)
+    def forward_features(self, x, fp8=False, bf16_residual=False):
+        """All tokens, no final norm (residual stream [B*N, D]: f32, or bf16 with bf16_residual); used
+        by the target encoder, whose final norm is fused into the JEPA loss kernel."""
+        t, _ = self.forward_ragged(x, None, final_norm=False, fp8=fp8, bf16_residual=bf16_residual and not fp8)
         return t
 
     def forward(self, x, masks=None):

@@ -34,7 +34,8 @@ def _sdpa_ref(q, kv, B, nq, N, H, hd):
 
 
 @pytest.mark.parametrize("B,nq,N,H,hd", [(3, 1, 2048, 16, 64), (2, 3, 1000, 16, 88), (2, 16, 77, 12, 32),
-                                         (2, 20, 300, 4, 64), (1, 1, 8192, 16, 64), (2, 2, 129, 2, 128)])
+                                         (2, 20, 300, 4, 64), (1, 1, 8192, 16, 64), (2, 2, 129, 2, 128),
+                                         (1, 16, 300, 2, 128), (1, 40, 130, 2, 120)])  # > 64 KB of LDS
 def test_xattn_fwd_vs_fp32(B, nq, N, H, hd):
     from vjepa2_amd import ops
 
@@ -53,7 +54,8 @@ def test_xattn_fwd_vs_fp32(B, nq, N, H, hd):
 
 
 @pytest.mark.parametrize("B,nq,N,H,hd", [(3, 1, 2048, 16, 64), (2, 3, 1000, 16, 88), (2, 16, 77, 12, 32),
-                                         (2, 3, 4600, 16, 80), (2, 37, 300, 4, 64)])
+                                         (2, 3, 4600, 16, 80), (2, 37, 300, 4, 64), (1, 16, 300, 2, 128),
+                                         (1, 40, 130, 2, 120)])
 def test_xattn_bwd_vs_fp32(B, nq, N, H, hd):
     from vjepa2_amd import ops
 

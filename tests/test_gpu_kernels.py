@@ -148,6 +148,23 @@ def test_gemm_epilogues(M, N):
     _close(dw, exp, 2e-4 * math.sqrt(M), 1e-5, "wgrad accumulate")
 
 
+@pytest.mark.parametrize("two_wg", ["0", "1"])
+def test_gemm_bf16_resid_tile_paths(two_wg, monkeypatch):
+    """EPI_BF16_RESID through the LDS-staged epilogue (8-wave, 128-wide tiles: VJ_GEMM_2W=0) and the
+    two-workgroup direct-store kernel (VJ_GEMM_2W=1), N = 384 (not a multiple of 256)."""
+    from vjepa2_amd import ops
+
+    monkeypatch.setenv("VJ_GEMM_2W", two_wg)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    M, N, K = 1333, 384, 320
+    X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
+    b = torch.randn(N, generator=g).to(DEV)
+    r = torch.randn(M, N, generator=g).to(DEV).bfloat16()
+    y = ops.linear_fwd(X, W, b, ops.EPI_BF16_RESID, resid=r)
+    _close(y, X.float() @ W.float().t() + b + r.float(), 1e-3, 8e-3, f"EPI_BF16_RESID (2W={two_wg})")
+
+
 @pytest.mark.parametrize("knobs", [dict(VJ_GEMM_PXCD="1"), dict(VJ_GEMM_PXCD="3", VJ_GEMM_GROUP="3")])
 def test_gemm_persistent_walk(knobs, monkeypatch):
     """The 256-row kernel is persistent: with few blocks per XCD every block walks many tiles, which

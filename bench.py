@@ -1,6 +1,6 @@
 """Benchmark: V-JEPA 2 ViT-L/16 16x256^2 JEPA train step (fwd + bwd + AdamW + EMA), bf16, synthetic.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]      (N > 1: starts N rank processes itself)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...   (one rank per GPU)
 
 Workload (BASELINE.json configs[1]; per-GPU batch 24 = configs/train/vitl16/pretrain-256px-16f.yaml):
@@ -75,6 +75,9 @@ def main():
     ap.add_argument("--kernel-events", type=int, default=1)
     ap.add_argument("--fp8-target", type=int, default=0, help="target encoder QKV / fc1 GEMMs on the fp8 MFMA")
     args = ap.parse_args()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        # no launcher: start one rank process per GPU from this GPU-free parent
+        sys.exit(spawn_ranks(args.gpus))
 
     from vjepa2_amd import ops
     from vjepa2_amd.distributed import init_distributed
@@ -87,6 +90,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", 0)) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     world, rank = init_distributed()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} rank(s)")
     dev = torch.device("cuda", local_rank)
     B, T, S = args.batch, args.frames, args.crop
     N = (T // 2) * (S // 16) ** 2
@@ -145,9 +150,14 @@ def main():
     torch.cuda.synchronize()
     if prof:
         prof.start()
+    # step-boundary events on the compute stream (no host sync between steps): per-step times for
+    # the median; the contract's ms_per_step stays wall-clock over the K steps
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
+    marks[0].record()
     for i in range(args.warmup, nsteps):
         loss = run(i)
+        marks[i - args.warmup + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -159,6 +169,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     ms = elapsed * 1000.0 / args.steps
+    per_step = sorted(a.elapsed_time(b) for a, b in zip(marks[:-1], marks[1:]))
+    ms_median = per_step[len(per_step) // 2] if len(per_step) % 2 else 0.5 * (
+        per_step[len(per_step) // 2 - 1] + per_step[len(per_step) // 2])
+    if world > 1:
+        t = torch.tensor([ms_median], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms_median = t.item()
     total_clips = B * world * args.steps
     value = total_clips / elapsed
     flops = sum(step_flops(args.model, B, N, d[1], d[2]) for d in data[args.warmup:]) / args.steps
@@ -212,7 +229,10 @@ def main():
                                       "train step: target fwd + ctx fwd/bwd (2 masks) + predictor fwd/bwd + L1 + "
                                       "AdamW + EMA", "model": args.model, "global_batch": B * world,
                           "seq_len": N, "parallelism": f"dp{world}"},
-               "clips_per_s_per_gpu": round(value / world, 3), "step_tflop": round(flops / 1e12, 2),
+               "value_is": "whole-job clips/s (all ranks' clips / max-over-ranks time); per GPU: clips_per_s_per_gpu",
+               "clips_per_s_per_gpu": round(value / world, 3), "ms_per_step_median": round(ms_median, 2),
+               "clips_per_s_per_gpu_median": round(B / (ms_median * 1e-3), 3),
+               "dist_backend": dist.get_backend() if world > 1 else None, "step_tflop": round(flops / 1e12, 2),
                "step_tflops_per_gpu": round(flops / (ms * 1e-3) / 1e12, 1),
                "mfu_bf16": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                "loss_last": round(float(loss.item()), 5), "roofline": roof, "cpu_baseline": cpu}
@@ -223,6 +243,45 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without torchrun: one child process per rank (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in its env), started before this process makes any HIP call
+    (torch.cuda.device_count() does not initialise the runtime). Returns the exit code: the first
+    failing rank's, after terminating the others."""
+    import socket
+    import subprocess
+
+    backend = os.environ.get("VJ_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and ndev < n:
+        print(f"bench.py --gpus {n}: RCCL needs one device per rank but {ndev} HIP device(s) are visible "
+              f"(VJ_DIST_BACKEND=gloo rehearses {n} ranks on fewer devices)", file=sys.stderr, flush=True)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    code = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            try:
+                rc = p.wait(timeout=1.0)
+            except subprocess.TimeoutExpired:
+                continue
+            alive.remove(p)
+            if rc != 0 and code == 0:
+                code = rc if rc > 0 else 1
+                for q in alive:
+                    q.terminate()
+    return code
 
 
 def _pmc_traffic(label, workload):

@@ -380,7 +380,7 @@ def test_rope_fwd_bwd(hd, H):
 
 @pytest.mark.parametrize("M", [300, 1500])
 @pytest.mark.parametrize("hd,H", [(64, 2), (32, 3), (80, 2), (88, 1), (32, 12)])
-def test_fused_rope_paths(M, hd, H):
+def test_fused_rope_paths(M, hd, H, monkeypatch):
     """QKV GEMM with RoPE fused into the epilogue vs fp32 GEMM + oracle RoPE (M >= 1024: one bf16
     rounding of the fp32 result, <= 1 ulp; M < 1024 takes GEMM -> bf16 -> rope -> bf16, two
     roundings, so the bound is 1 ulp of the rotated inputs). Attention backward with the inverse
@@ -396,6 +396,12 @@ def test_fused_rope_paths(M, hd, H):
     w = (0.1 * torch.randn(3 * D, K, generator=g)).to(DEV).bfloat16()
     b = torch.randn(3 * D, generator=g).to(DEV)
     fused = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
+    if M >= 1024:  # ping-pong kernel == one-tile-per-workgroup kernel, bitwise
+        for pp in ("1", "0"):
+            monkeypatch.setenv("VJ_GEMM_PP", pp)
+            other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
+            assert torch.equal(fused, other), f"qkv_rope: VJ_GEMM_PP={pp} differs from the default kernel"
+        monkeypatch.delenv("VJ_GEMM_PP")
     # expected: our own f32 GEMM (same accumulation), RoPE in fp32 by the oracle
     y32 = ops.linear_fwd(x, w, b, ops.EPI_F32).cpu()
     idl = ids.cpu().long()[None]
@@ -589,3 +595,53 @@ def test_adamw_ema_match_oracle():
     torch.cuda.synchronize()
     _close(td, t, 1e-7, 1e-6, "ema")
     assert torch.equal(tbf, td.bfloat16())
+
+
+@pytest.mark.parametrize("K", [64, 192, 256, 1024])
+@pytest.mark.parametrize("pxcd", [None, "1", "3"])
+def test_gemm_pingpong_matches_one_tile_kernel(K, pxcd, monkeypatch):
+    """The ping-pong kernel (vj_gemm_pp.hip: two wave groups alternating K-loop / epilogue over one
+    LDS ring) against the one-tile-per-workgroup kernel (VJ_GEMM_PP=0) on every epilogue: the same
+    per-wave tile and K order, so the outputs are BITWISE equal; and against fp32 math. K = 64 / 128
+    make one / two K-tiles per tile (the group hand-over DMAs span tiles); VJ_GEMM_PXCD = 1 / 3 puts
+    many tiles on each block (many periods, odd and even counts) and N = 200 a ragged last column.
+    K = 64 / 128 (fewer K-tiles than the ring's 3 stages) take the one-tile kernel: trivially equal."""
+    from vjepa2_amd import ops
+
+    if pxcd:
+        monkeypatch.setenv("VJ_GEMM_PXCD", pxcd)
+    g = torch.Generator(device="cpu").manual_seed(K)
+    for M, N in [(2100, 384), (1333, 200)]:
+        X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+        W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
+        b = torch.randn(N, generator=g).to(DEV)
+        resid = torch.randn(M, N, generator=g).to(DEV)
+        dgs = torch.randn(M, N, generator=g).to(DEV).bfloat16()
+        ref = X.float() @ W.float().t() + b
+
+        def run():
+            outs = {"bf16": ops.linear_fwd(X, W, b, ops.EPI_BF16),
+                    "f32": ops.linear_fwd(X, W, b, ops.EPI_F32),
+                    "f32_resid": ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid),
+                    "bf16_resid": ops.linear_fwd(X, W, b, ops.EPI_BF16_RESID, resid=resid.bfloat16())}
+            d, a = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
+            outs["gelu_d"], outs["gelu_a"] = d, a
+            outs["gelu_nosave"] = ops.linear_fwd(X, W, b, ops.EPI_GELU)[1]
+            gb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(M, N, K, X, K, True, W, K, True, ops.EPI_GELU_BWD, out=gb, ldc=N, aux=dgs, ldaux=N)
+            outs["gelu_bwd"] = gb
+            torch.cuda.synchronize()
+            return {k: v.detach().clone() for k, v in outs.items()}
+
+        monkeypatch.setenv("VJ_GEMM_PP", "1")
+        pp = run()
+        monkeypatch.setenv("VJ_GEMM_PP", "0")
+        one = run()
+        monkeypatch.delenv("VJ_GEMM_PP")
+        for k in pp:
+            assert torch.equal(pp[k], one[k]), f"ping-pong != one-tile kernel: {k} M={M} N={N} K={K} pxcd={pxcd}"
+        _close(pp["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "pp EPI_F32")
+        _close(pp["f32_resid"], ref + resid, 1e-4 * math.sqrt(K) * 4, 1e-4, "pp EPI_F32_RESID")
+        _close(pp["bf16"], ref, 1e-3, 8e-3, "pp EPI_BF16")
+        assert torch.equal(pp["gelu_a"], pp["gelu_nosave"])
+        _close(pp["gelu_bwd"], (X.float() @ W.float().t()) * dgs.float(), 2e-3, 1.5e-2, "pp EPI_GELU_BWD")

@@ -51,3 +51,25 @@ def test_train_step_vs_oracle(bf16_target):
           f"AdamW update sign agreement {agree:.4f}")
     assert rel < 1e-2
     assert agree > 0.9
+
+
+def test_target_residual_precision_follows_mixed_precision(monkeypatch):
+    """The target encoder's bf16 residual stream is the reference's autocast precision, so it is the
+    default only under bf16 mixed precision: a float32 config (mixed_precision False, the reference
+    runs forward_target in f32) keeps the residual in f32; VJ_TARGET_BF16=0 turns it off."""
+    from vjepa2_amd.train import JEPATrainer, init_opt, init_video_model
+
+    def trainer(mp):
+        torch.manual_seed(239)
+        enc, pred = init_video_model(device="cuda", patch_size=16, max_num_frames=4, tubelet_size=2,
+                                     model_name="vit_small", crop_size=32, pred_depth=1, pred_num_heads=12,
+                                     pred_embed_dim=384, use_mask_tokens=True, num_mask_tokens=2, use_rope=True)
+        opt, _, _, _ = init_opt(enc, pred, iterations_per_epoch=1, start_lr=1e-4, ref_lr=1e-4, warmup=0,
+                                num_epochs=1, mixed_precision=mp)
+        return JEPATrainer(enc, pred, copy.deepcopy(enc), opt, mixed_precision=mp)
+
+    monkeypatch.delenv("VJ_TARGET_BF16", raising=False)
+    assert trainer(True).target_bf16_residual is True
+    assert trainer(False).target_bf16_residual is False
+    monkeypatch.setenv("VJ_TARGET_BF16", "0")
+    assert trainer(True).target_bf16_residual is False

@@ -14,7 +14,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvjepa_hip.so")
-SOURCES = ["vj_capi.hip", "vj_gemm.hip", "vj_gemm256.hip", "vj_attn.hip", "vj_ops.hip", "vj_f32.hip", "vj_xattn.hip"]
+SOURCES = ["vj_capi.hip", "vj_gemm.hip", "vj_gemm256.hip", "vj_gemm_pp.hip", "vj_attn.hip", "vj_ops.hip", "vj_f32.hip", "vj_xattn.hip"]
 ARCH = os.environ.get("VJEPA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (gfx950 allows it), so the softmax /
@@ -36,7 +36,7 @@ def _torch_libdir():
 
 
 def _needs_build(obj, src, extra=()):
-    deps = [src, os.path.join(CSRC, "vj_common.h"), *extra]
+    deps = [src, *[os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")], *extra]
     return not os.path.exists(obj) or any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 

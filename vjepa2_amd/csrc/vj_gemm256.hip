@@ -19,150 +19,14 @@
 // through a padded LDS image in the freed slot, with bias / residual / GELU / GELU' / RoPE fused.
 #include <stdlib.h>
 #include <type_traits>
-#include "vj_common.h"
-
-// m-tiles of residual / saved-derivative rows the direct epilogue keeps in flight
-#ifndef VJ_GEMM_AUX_PF
-#define VJ_GEMM_AUX_PF 1
-#endif
-// Waves that issue the LDS-DMA of a K stage: 8 (all) or 4 (waves 0-3, so their SIMD partners 4-7
-// keep the matrix pipe busy while the DMA issues)
-#ifndef VJ_GEMM_DMA_WAVES
-#define VJ_GEMM_DMA_WAVES 8
-#endif
+#include "vj_gemm_tile.h"
 
 namespace {
-
-// EPI_BF16_RESID: bf16 residual in (aux), bf16 out — the no-grad target encoder's residual stream in
-// the reference's own autocast precision (x = x + proj(...) in bf16), half the epilogue bytes of F32_RESID
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5, EPI_PARTIAL = 6,
-       EPI_BF16_RESID = 7 };
-
-using RopeP = VjRope;
-
-struct G256 {
-  const bf16_t* A;
-  const bf16_t* B;
-  int M, N, K;
-  long lda, ldb;
-  void* C;
-  long ldc;
-  void* C2;
-  long ldc2;
-  const float* bias;
-  const void* aux;
-  long ldaux;
-  int tiles_m, tiles_n;
-  RopeP rope;
-  int kslice;  // K range of one K slice (= K unless EPI_PARTIAL)
-  int nsplit;  // K slices: slice z covers [z*kslice, min(K, (z+1)*kslice)) (EPI_PARTIAL only; else 1)
-  float* ws;   // EPI_PARTIAL: f32 partial products [nsplit][M][N]
-  int group;   // tile rows per group of the grouped tile order (0: row-major, n fastest)
-  // F8 kernels: A / B are fp8 e4m3 (OCP) viewed as bf16 pairs (K, lda, ldb above in 2-byte units);
-  // ea[m] / eb[n] = power-of-two exponents of the per-row (A: token) / per-row (B: output channel)
-  // scales: A(m, k) = a8 * 2^ea[m], B(n, k) = b8 * 2^eb[n] (E8M0 scale operands of the MFMA)
-  const int* ea = nullptr;
-  const int* eb = nullptr;
-  int stagger = 0;  // s_sleep(32) units odd blocks of an XCD wait before their first tile
-};
-
-constexpr int BK = 64;
-// LDS behind the two operand stages for the per-kernel tables: the GELU tables (f32 derivative:
-// 13 KB) or the RoPE tile positions (1 KB) + interleaved cos/sin table (npos * half * 8 B).
-constexpr int TAB_BYTES = 16384;
-constexpr int ROPE_TAB_MAX = (TAB_BYTES - 256 * 4) / 8;  // cos/sin pairs that fit behind the positions
-
-__device__ __forceinline__ uint32_t clampb(long b) {
-  if (b < 0) return 0;
-  return b > 0x7fffffffL ? 0x7fffffffu : (uint32_t)b;
-}
-
-__device__ __forceinline__ int mn_swz(int k) { return 2 * (k & 3) + 8 * ((k >> 3) & 1); }
-
-// K-major image: [ROWS][64] bf16, 128-B rows, chunk ^= (row>>1)&7.
-// MN-major image: [64][ROWS] bf16, ROWS*2-B rows, chunk ^= mn_swz(k).
-// PERM (K-major B only): LDS row r of each WN-row group holds global row NTN*(r%16) + r/16 of the
-// group, so n-tile j of the MFMA accumulators covers the group's columns {NTN*c + j}: each lane
-// then owns NTN CONSECUTIVE output columns and the epilogue stores straight from registers.
-// NW waves issue the tile's 1-KB pieces (waves 0 .. NW-1).
-template <bool KMAJ, int ROWS, bool PERM = false, int NW = 8, int BKT = 64, int WNX = 4>
-__device__ __forceinline__ void stage(__amdgpu_buffer_rsrc_t rs, long ld, int rows_left, int k0, int K,
-                                      LDS_AS char* lds, int wave, int lane) {
-  constexpr int PIECES = ROWS * BKT * 2 / 1024;  // 1-KB DMA pieces per operand tile
-  constexpr int PPW = PIECES / NW;
-  static_assert(KMAJ || BKT == 64, "MN-major staging is written for 64-deep K tiles");
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int p = wave * PPW + i;
-    uint32_t voff;
-    if constexpr (KMAJ) {
-      // 128-B rows (BK 64): chunk ^= (row>>1)&7; 64-B rows (BK 32): chunk ^= (row>>2)&3
-      constexpr int CPR = BKT / 8, RPP = 64 / CPR;  // 16-B chunks per row, rows per piece
-      const int r = p * RPP + lane / CPR;
-      const int c = (lane % CPR) ^ (BKT == 64 ? ((r >> 1) & 7) : ((r >> 2) & 3));
-      const int kk = k0 + c * 8;
-      int gr = r;
-      if constexpr (PERM) {
-        constexpr int WN = ROWS / WNX, NTN = WN / 16;
-        const int rl = r % WN;
-        gr = (r - rl) + NTN * (rl & 15) + (rl >> 4);
-      }
-      voff = (gr < rows_left && kk < K) ? (uint32_t)(((long)gr * ld + kk) * 2) : VJ_OOB;
-    } else {
-      constexpr int CPR = ROWS / 8;     // chunks per LDS row
-      constexpr int RPP = 64 / CPR;     // k-rows per piece
-      const int kr = p * RPP + lane / CPR;
-      const int c = (lane % CPR) ^ mn_swz(kr);
-      const int col = c * 8;
-      voff = (k0 + kr < K && col < rows_left) ? (uint32_t)(((long)(k0 + kr) * ld + col) * 2) : VJ_OOB;
-    }
-    dma16(rs, lds + p * 1024, voff);
-  }
-}
-
-// 16x16x32 operand fragment: lane l holds X(rb + (l&15), 32s + 8(l>>4) + j), j = 0..7.
-template <bool KMAJ, int ROWS, int BKT = 64>
-__device__ __forceinline__ bf16x8 frag(const LDS_AS char* lds, int rb, int s, int lane) {
-  if constexpr (KMAJ) {
-    const int r = rb + (lane & 15);
-    if constexpr (BKT == 32) {  // 64-B rows, one k-step
-      const int c = (lane >> 4) ^ ((r >> 2) & 3);
-      return *(const LDS_AS bf16x8*)(lds + r * 64 + c * 16);
-    }
-    const int c = (4 * s + (lane >> 4)) ^ ((r >> 1) & 7);
-    return *(const LDS_AS bf16x8*)(lds + r * 128 + c * 16);
-  } else {
-    const int gi = lane & 15;
-    const int k0 = 32 * s + 8 * (lane >> 4) + (gi >> 2);
-    const int col = rb + 4 * (gi & 3);
-    const int within = (col & 7) * 2;
-    const int c = col >> 3;
-    const s16x4 lo = ds_read_tr16_async(lds + k0 * (ROWS * 2) + ((c ^ mn_swz(k0)) * 16) + within);
-    const s16x4 hi = ds_read_tr16_async(lds + (k0 + 4) * (ROWS * 2) + ((c ^ mn_swz(k0 + 4)) * 16) + within);
-    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  }
-}
-
-// GELU (nn.GELU(), vision_transformer.py:100) in the epilogues: the forward evaluates it on the bf16
-// pre-activation (the reference's autocast order) and, when the caller saves for the backward, the
-// derivative gelu'(pre) in the same pass (its erf and Gaussian terms are already computed); the
-// backward epilogue then multiplies by the saved derivative (one VALU op per element).
-__device__ __forceinline__ uint32_t gelu_pair(uint32_t pk, uint32_t* dpk) {
-  float y0, d0, y1, d1;
-  gelu_fwd_grad(__builtin_bit_cast(float, pk << 16), y0, d0);
-  gelu_fwd_grad(__builtin_bit_cast(float, pk & 0xffff0000u), y1, d1);
-  if (dpk) *dpk = pack_bf2(d0, d1);
-  return pack_bf2(y0, y1);
-}
 
 #if VJ_GEMM_STAMPS  // diagnostic build: s_memtime per tile (start, main loop done, epilogue done) of wave 0
 __device__ long vj_gemm_stamps[2048 * 16 * 4];
 #endif
 
-struct Tile {
-  int m0, n0, z, Keff, nk;  // buffer descriptors are rebuilt per DMA: SGPRs are the scarce resource
-};
 
 // NWV = 8: 8 waves (2 x 4), 64-deep K tiles, one workgroup per CU. NWV = 4 ("2W"): 4 waves (2 x 2),
 // 32-deep K tiles, 64 KB of LDS, TWO workgroups per CU, so one workgroup's epilogue (HBM / VALU)
@@ -1024,6 +888,11 @@ int launch256(int epi, const G256& g, hipStream_t st) {
 
 }  // namespace
 
+bool vj_gemm_pp_enabled();
+int vj_gemm_pp_dispatch(int M, int N, int K, const void* A, long lda, const void* B, long ldb, int epi,
+                        const float* bias, const void* aux, long ldaux, void* C, long ldc, void* C2, long ldc2,
+                        hipStream_t st, const void* rope, int group, int grid);
+
 // Called by vj_gemm_bf16_splitk (splitk == 1) when the problem suits a 256-row tile; arguments
 // already validated there. Returns VJ_ERR_UNSUPPORTED when it declines.
 int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
@@ -1033,6 +902,13 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
     return VJ_ERR_UNSUPPORTED;
   if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
     return VJ_ERR_UNSUPPORTED;
+  // K-major A and B: the ping-pong kernel (vj_gemm_pp.hip) when it takes the shape
+  if (a_kmajor && b_kmajor && vj_gemm_pp_enabled()) {
+    const int tm = vj_cdiv(M, 256), tn = vj_cdiv(N, 128);
+    const int rc = vj_gemm_pp_dispatch(M, N, K, A, lda, B, ldb, epi, bias, aux, ldaux, C, ldc, C2, ldc2, st, rope,
+                                       tile_group(tm, tn), grid256((long)tm * tn));
+    if (rc != VJ_ERR_UNSUPPORTED) return rc;
+  }
   // 256-wide tiles (direct-store epilogue) unless the last column tile would waste > 15 % of the work
   // (measured, tools/bench_kernels.py: predictor QKV N = 1152 -17 % with 256-wide tiles; N = 384 +14 %)
   const bool wide = N % 256 == 0 || (N > 256 && (vj_cdiv(N, 256) * 256L * 100 <= 115L * N || force_bn256()));

@@ -111,10 +111,14 @@ class TokenLayout:
 # Transformer block (modules.py:500-563): x + attn(LN1 x); x + mlp(LN2 x)
 
 
-def _attn_scale(attn, hd):
+def _attn_scale(attn, hd, lay=None):
     # F.scaled_dot_product_attention uses the default 1/sqrt(hd) (modules.py:367-372); the non-SDPA
-    # branch uses attn.scale (= qk_scale or hd^-0.5).
-    return hd**-0.5 if attn.use_sdpa else attn.scale
+    # branch uses attn.scale (= qk_scale or hd^-0.5). With the frame-causal attn_mask (lay.fblk > 0,
+    # the AC predictor) ACRoPEAttention always takes the SDPA branch (modules.py:243-247), whatever
+    # use_sdpa says, so the scale is SDPA's default there too.
+    if attn.use_sdpa or (lay is not None and lay.fblk > 0):
+        return hd**-0.5
+    return attn.scale
 
 
 def _resid_epi(x):
@@ -138,7 +142,7 @@ def block_forward_fp8(x, blk, lay):
         qkv = ops.qkv_rope_fp8(ln1, e1, w8, ew, attn.qkv.bias, H, hd, lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
     else:
         qkv = ops.linear_fwd_fp8(ln1, e1, w8, ew, attn.qkv.bias, EPI_BF16)
-    o, _ = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd), fblk=lay.fblk)
+    o, _ = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd, lay), fblk=lay.fblk)
     x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, _resid_epi(x), resid=x)
     ln2, e2 = ops.layernorm_fwd_fp8(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
     w18, ew1 = weight_fp8(mlp.fc1.weight)
@@ -159,7 +163,7 @@ def block_forward(x, blk, lay, save):
                            lay.tpr, c, s)
     else:
         qkv = ops.linear_fwd(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
-    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd), fblk=lay.fblk)
+    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd, lay), fblk=lay.fblk)
     x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, _resid_epi(x), resid=x)
     ln2, m2, r2 = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, want_stats=save)
     hidden = mlp.fc1.weight.shape[0]
@@ -244,7 +248,7 @@ def block_backward(dxo, blk, lay, saved):
     if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
-    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope, fblk=lay.fblk)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk)
     dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
     ops.linear_wgrad(dqkv, ln1, grad_buf(attn.qkv.weight))
     _bias_grad(attn.qkv, dqkv)
@@ -306,7 +310,7 @@ def attn_module_forward(x, attn, lay):
                            lay.tpr, c, s)
     else:
         qkv = ops.linear_fwd(x, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
-    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd), fblk=lay.fblk)
+    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd, lay), fblk=lay.fblk)
     y = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32)
     return y, (x, qkv, o, stats)
 
@@ -323,7 +327,7 @@ def attn_module_backward(dy, attn, lay, saved):
     if attn.use_rope:
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
-    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd), rope=rope, fblk=lay.fblk)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk)
     dx = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
     ops.linear_wgrad(dqkv, x, grad_buf(attn.qkv.weight))
     _bias_grad(attn.qkv, dqkv)

@@ -120,10 +120,11 @@ class JEPATrainer:
         # opt-in: the no-grad target encoder's QKV / fc1 GEMMs on the fp8 MFMA (functions.block_forward_fp8)
         self.fp8_target = fp8_target
         # the no-grad target encoder's residual stream in bf16 (the reference's autocast precision;
-        # half the bytes of its proj / fc2 epilogues and LayerNorm reads). Default on; env
+        # half the bytes of its proj / fc2 epilogues and LayerNorm reads). Default on under bf16
+        # mixed precision (the reference's forward_target runs under autocast there); env
         # VJ_TARGET_BF16=0 or target_bf16_residual=False keeps it f32.
-        if target_bf16_residual is None:
-            target_bf16_residual = os.environ.get("VJ_TARGET_BF16", "1") != "0"
+        if target_bf16_residual is None:  # float32 configs (mixed_precision False) keep the reference's f32
+            target_bf16_residual = mixed_precision and os.environ.get("VJ_TARGET_BF16", "1") != "0"
         self.target_bf16_residual = bool(target_bf16_residual)
         enc_w, pred_w, enc_n, pred_n = optimizer.arenas
         device = enc_w.data.device

@@ -27,16 +27,23 @@ int vj_version(void);
 int vj_get_last_error(char* buf, size_t n);
 int vj_device_sync(void);
 
-/* GEMM epilogues */
+/* GEMM epilogues. vj_gemm_bf16 accepts 0-4 and 7; 5 and 6 are internal (5: vj_qkv_rope_gemm's RoPE
+ * epilogue, 6: the split-K partial slabs of vj_gemm_bf16_splitk) and are rejected there. */
 enum {
-  VJ_EPI_BF16 = 0,      /* C(bf16) = acc + bias                                           */
-  VJ_EPI_F32 = 1,       /* C(f32)  = acc + bias                                           */
-  VJ_EPI_F32_RESID = 2, /* C(f32)  = aux(f32 residual) + acc + bias   (Block residual add) */
-  VJ_EPI_GELU = 3,      /* C(bf16) = pre = acc + bias (optional), C2(bf16) = GELU_erf(pre) */
-  VJ_EPI_GELU_BWD = 4   /* C(bf16) = acc * GELU'(aux bf16 pre-activation)                 */
+  VJ_EPI_BF16 = 0,       /* C(bf16) = acc + bias                                                      */
+  VJ_EPI_F32 = 1,        /* C(f32)  = acc + bias                                                      */
+  VJ_EPI_F32_RESID = 2,  /* C(f32)  = aux(f32 residual) + acc + bias   (Block residual add)            */
+  VJ_EPI_GELU = 3,       /* C(bf16) = GELU'(pre) if C != NULL, C2(bf16) = GELU_erf(pre), pre = bf16(acc + bias) */
+  VJ_EPI_GELU_BWD = 4,   /* C(bf16) = acc * aux (the saved bf16 GELU'(pre))                             */
+  VJ_EPI_ROPE = 5,       /* internal: QKV + 3-axis RoPE (vj_qkv_rope_gemm)                               */
+  VJ_EPI_PARTIAL = 6,    /* internal: f32 split-K partial slabs (vj_gemm_bf16_splitk)                    */
+  VJ_EPI_BF16_RESID = 7  /* C(bf16) = bf16(aux(bf16 residual) + acc + bias) (no-grad target encoder)    */
 };
 
-/* C[m,n] = sum_k A(m,k) B(n,k) (+ epilogue), bf16 operands, f32 accumulate (MFMA 32x32x16).
+/* C[m,n] = sum_k A(m,k) B(n,k) (+ epilogue), bf16 operands, f32 accumulate. M >= 1024 runs the 256-row
+ * tile kernels on v_mfma_f32_16x16x32_bf16 (vj_gemm256.hip; vj_gemm_pp.hip, the two-wave-group
+ * ping-pong, for the K-major RoPE epilogue by default, VJ_GEMM_PP / VJ_GEMM_PP_EPIS select it), smaller
+ * M the 128-row kernel on v_mfma_f32_32x32x16_bf16 (vj_gemm.hip).
  * A(m,k) = a_kmajor ? A[m*lda+k] : A[k*lda+m];  B(n,k) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n].
  * Replaces nn.Linear forward/backward (modules.py:77-83, 330, 379-381; predictor.py:182, 244) and the
  * Conv3d tubelet projection as a GEMM over im2col rows (patch_embed.py:42-52). */
@@ -50,7 +57,8 @@ int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmaj
                         int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
                         void* C2, long ldc2, int splitk, float* ws, long ws_floats, void* stream);
 
-/* Varlen non-causal flash attention, head_dim 32 or 64 (F.scaled_dot_product_attention,
+/* Varlen non-causal flash attention, head_dim 32, 64, 80 or 88 (80 / 88 padded to 96 in LDS and in the
+ * MFMA loops; F.scaled_dot_product_attention,
  * modules.py:367-372 / 411-418). Tokens of `ngroups` groups of equal-length sequences are
  * concatenated: group g has nseq[g] sequences of len[g] tokens. q/k/v at columns q_off/k_off/v_off
  * + h*hd of the [T, ld] bf16 buffer; O bf16 [T, ldo] at column h*hd.
@@ -199,7 +207,7 @@ int vj_video_transform(int B, int T, int H, int W, int C, int S, const void* fra
  * q bf16 [B*nq][ldq] (head h at column h*hd), kv bf16 [B*N][ldkv] (k at h*hd, v at H*hd + h*hd: the
  * reference's kv Linear output reshaped (B, N, 2, H, hd)), o bf16 [B*nq][ldo]; lse2 f32 [B*H][nq] =
  * log2-domain log-sum-exp of scale*log2(e)*q.k, kept for the backward. hd % 8 == 0, hd <= 128.
- * ws: f32 workspace of vj_xattn_ws_floats() floats (split-KV partials, 128 keys per chunk). */
+ * ws: f32 workspace of vj_xattn_ws_floats() floats (split-KV partials, 64 keys per chunk). */
 int vj_xattn_ws_floats(int B, int nq, int N, int H, int hd, long* out);
 int vj_xattn_fwd(int B, int nq, int N, int H, int hd, const void* q, long ldq, const void* kv, long ldkv, void* o,
                  long ldo, float* lse2, float scale, float* ws, long ws_floats, void* stream);

@@ -282,8 +282,28 @@ class OracleTrainer:
              for zi, mx, my in zip(z, masks_enc, masks_pred)]
         return jepa_loss(z, h, masks_pred, self.loss_exp)
 
+    def loss_groups(self, groups):
+        """train.py:414-435 with several frames-per-clip groups [(clips, masks_enc, masks_pred), ...]:
+        group i's predictor uses mask token i (wrappers.py:36-43, mask_index = i) and the loss is the
+        mean over every (group, mask) pair (train.py:429-434)."""
+        tot, n = 0.0, 0
+        for i, (clips, me, mp) in enumerate(groups):
+            with torch.no_grad():
+                h = forward_target(clips, self.tgt, self.enc_cfg)
+            z = [encoder_forward(clips, self.enc, self.enc_cfg, masks=m) for m in me]
+            z = [predictor_forward(zi, mx, my, self.pred, self.pred_cfg, mask_index=i)
+                 for zi, mx, my in zip(z, me, mp)]
+            tot = tot + jepa_loss(z, h, mp, self.loss_exp) * len(me)
+            n += len(me)
+        return tot / n
+
+    def step_groups(self, groups, lr, wd, momentum):
+        return self._update(self.loss_groups(groups), lr, wd, momentum)
+
     def step(self, clips, masks_enc, masks_pred, lr, wd, momentum):
-        loss = self.loss(clips, masks_enc, masks_pred)
+        return self._update(self.loss(clips, masks_enc, masks_pred), lr, wd, momentum)
+
+    def _update(self, loss, lr, wd, momentum):
         loss.backward()
         with torch.no_grad():
             for sd in (self.enc, self.pred):

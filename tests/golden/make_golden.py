@@ -127,6 +127,33 @@ def gen_encoder():
                   outs=[o.detach() for o in outs], gys=gys, gparams=grads_of(enc)))
 
 
+def gen_vitl_autocast():
+    """The reference ViT-L/16 (vision_transformer.py:275 vit_large, RoPE, uniform_power) at 16 frames of
+    64^2 (N = 128 tokens, one clip), seeded init, run twice on the same input: in fp32 and under
+    torch.autocast("cpu", bfloat16) (the reference's own bf16 precision: bf16 Linear / SDPA operands,
+    RoPE angles in bf16, LayerNorm in f32). Stores the seed, the input, both outputs and per-tensor
+    sums of the initial weights (the GPU test rebuilds the same weights from the seed and checks them
+    against these sums before comparing outputs): no weights in the fixture."""
+    seed = 239
+    torch.manual_seed(seed)
+    enc = vit.vit_large(img_size=64, num_frames=16, tubelet_size=2, use_rope=True, uniform_power=True,
+                        use_sdpa=True)
+    enc.eval()
+    g = torch.Generator().manual_seed(240)
+    x = torch.randn(1, 3, 16, 64, 64, generator=g)
+    mask = sorted_unique_rows(1, 48, 128, g)  # a context pass: 48 kept tokens of 128
+    with torch.no_grad():
+        full32 = enc(x)
+        ctx32 = enc(x, masks=[mask])
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            full16 = enc(x)
+            ctx16 = enc(x, masks=[mask])
+    sums = {k: float(v.double().sum()) for k, v in enc.state_dict().items()}
+    save("vitl_autocast.pt", dict(seed=seed, x=x, mask=mask, full_f32=full32, ctx_f32=ctx32,
+                                  full_bf16=full16.float(), ctx_bf16=ctx16.float(), param_sums=sums,
+                                  cfg=dict(model="vit_large", img_size=64, num_frames=16, tubelet_size=2)))
+
+
 def gen_predictor():
     torch.manual_seed(11)
     pred = vpred.vit_predictor(img_size=32, use_mask_tokens=True, patch_size=16, num_frames=4, tubelet_size=2,
@@ -499,3 +526,4 @@ if __name__ == "__main__":
     gen_pooler()
     gen_multiclip()
     gen_ac_predictor()
+    gen_vitl_autocast()

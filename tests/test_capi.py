@@ -38,6 +38,17 @@ def test_library_exports_every_declared_symbol():
     assert set(_lib.SIGNATURES) == set(declared()), "ctypes signatures out of sync with the header"
 
 
+def test_header_enums_match_host_constants():
+    """The epilogue enum of include/vjepa_hip.h carries the same values as vjepa2_amd/ops.py's EPI_*."""
+    from vjepa2_amd import ops
+
+    src = open(HEADER).read()
+    enum = dict((k, int(v)) for k, v in re.findall(r"VJ_(EPI_\w+)\s*=\s*(\d+)", src))
+    host = {k: getattr(ops, k) for k in dir(ops) if re.fullmatch(r"EPI_[A-Z0-9_]+", k) and isinstance(getattr(ops, k), int)}
+    assert enum == host, (enum, host)
+    assert ops.EPI_NAMES[ops.EPI_BF16_RESID] == "EPI_BF16_RESID"
+
+
 def test_library_metadata_and_errors():
     from vjepa2_amd import _lib
 
@@ -46,6 +57,9 @@ def test_library_metadata_and_errors():
     # argument validation happens before any device work -> usable without a GPU
     rc = lib.vj_gemm_bf16(16, 16, 12, None, 16, 1, None, 16, 1, 0, None, None, 0, None, 16, None, 0, None)
     assert rc != 0 and "null operand" in _lib.last_error()
+    for internal in (5, 6):  # RoPE / split-K partial epilogues are internal: rejected at the C ABI
+        rc = lib.vj_gemm_bf16(16, 16, 16, None, 16, 1, None, 16, 1, internal, None, None, 0, None, 16, None, 0, None)
+        assert rc != 0 and "not a public epilogue" in _lib.last_error()
     rc = lib.vj_attn_fwd(10, 2, 48, None, 288, 0, 96, 192, None, 96, None, 0.1, 1, _lib.int_array([1]),
                          _lib.int_array([10]), None)
     assert rc != 0 and "head_dim" in _lib.last_error()

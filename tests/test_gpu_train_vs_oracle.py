@@ -73,3 +73,56 @@ def test_target_residual_precision_follows_mixed_precision(monkeypatch):
     assert trainer(False).target_bf16_residual is False
     monkeypatch.setenv("VJ_TARGET_BF16", "0")
     assert trainer(True).target_bf16_residual is False
+
+
+def test_two_fpc_groups_vs_oracle():
+    """Several frames-per-clip groups in one step (data.dataset_fpcs with distinct values, e.g.
+    [8, 4]): the MaskCollator yields one (clips, masks) entry per group; the reference runs the
+    wrappers' per-group loop (wrappers.py:20-43, predictor mask_index = group) and averages the loss
+    over every (group, mask) pair (train.py:425-435). HIP fused step vs the CPU oracle's
+    step_groups on the same weights / clips / masks: loss within 1e-2 relative, AdamW update signs."""
+    from vjepa2_amd.masks import MaskCollator
+    from vjepa2_amd.train import JEPATrainer, init_opt, init_video_model
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(239)
+    S, B = 64, 2
+    enc, pred = init_video_model(device=dev, patch_size=16, max_num_frames=8, tubelet_size=2, model_name="vit_small",
+                                 crop_size=S, pred_depth=2, pred_num_heads=12, pred_embed_dim=384, uniform_power=True,
+                                 use_mask_tokens=True, num_mask_tokens=4, zero_init_mask_tokens=False, use_sdpa=True,
+                                 use_rope=True)
+    enc_sd = {k: v.detach().cpu().clone() for k, v in enc.backbone.state_dict().items()}
+    pred_sd = {k: v.detach().cpu().clone() for k, v in pred.backbone.state_dict().items()}
+    tgt = copy.deepcopy(enc)
+    opt, _, _, _ = init_opt(enc, pred, iterations_per_epoch=10, start_lr=1e-4, ref_lr=1e-4, warmup=0, num_epochs=1,
+                            wd=0.04, final_wd=0.04, mixed_precision=True)
+    for g in opt.param_groups:
+        g["lr"] = 1e-4
+        if not g.get("WD_exclude", False):
+            g["weight_decay"] = 0.04
+    tr = JEPATrainer(enc, pred, tgt, opt, mixed_precision=True)
+    masks = [dict(aspect_ratio=[0.75, 1.5], num_blocks=8, spatial_scale=[0.15, 0.15], temporal_scale=[1.0, 1.0]),
+             dict(aspect_ratio=[0.75, 1.5], num_blocks=2, spatial_scale=[0.7, 0.7], temporal_scale=[1.0, 1.0])]
+    torch.manual_seed(0)
+    batch = [(0, 0, [torch.arange(8)])] * B + [(0, 0, [torch.arange(4)])] * B
+    groups = MaskCollator(masks, [8, 4], crop_size=S, patch_size=16)(batch)
+    assert len(groups) == 2
+    gen = torch.Generator().manual_seed(1)
+    clips = [torch.randn(B, 3, T, S, S, generator=gen) for T in (8, 4)]
+    tok0 = [t.detach().cpu().clone() for t in tr.mask_tokens]
+    loss = tr.train_step([c.to(dev) for c in clips], [[m.to(dev) for m in g[1]] for g in groups],
+                         [[m.to(dev) for m in g[2]] for g in groups], 0.99925).item()
+    ref = orc.OracleTrainer(enc_sd, pred_sd, dict(patch_size=16, tubelet_size=2, num_heads=6, depth=12, use_rope=True),
+                            dict(num_heads=12, depth=2, use_rope=True, grid_size=S // 16, num_mask_tokens=4,
+                                 num_patches=4 * (S // 16) ** 2))
+    ref_loss = ref.step_groups([(c, g[1], g[2]) for c, g in zip(clips, groups)], 1e-4, 0.04, 0.99925)
+    rel = abs(loss - ref_loss) / abs(ref_loss)
+    w = enc.backbone.blocks[0].attn.qkv.weight.detach().cpu()
+    w0 = enc_sd["blocks.0.attn.qkv.weight"]
+    agree = (torch.sign(w - w0) == torch.sign(ref.enc["blocks.0.attn.qkv.weight"].detach() - w0)).float().mean().item()
+    print(f"2 fpc groups: loss {loss:.6f} vs oracle {ref_loss:.6f} (rel {rel:.2e}), update sign agreement {agree:.4f}")
+    assert rel < 1e-2 and agree > 0.9
+    # mask tokens 0 and 1 (one per group) took a step; tokens 2 and 3 (unused) did not move
+    for i, t in enumerate(tr.mask_tokens):
+        moved = not torch.equal(t.detach().cpu(), tok0[i])
+        assert moved == (i < 2), f"mask token {i}: moved={moved}"

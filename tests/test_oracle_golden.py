@@ -197,3 +197,18 @@ def test_ac_predictor_golden(which):
         close(ins["ext"].grad, g["gext"], 1e-5, "dext")
     for n, v in g["gparams"].items():
         close(sd[n].grad, v, 1e-5, f"{which} d{n}")
+
+
+def test_vitl_seeded_init_matches_reference():
+    """vjepa2_amd.vision_transformer.vit_large under torch.manual_seed(239) builds the reference's
+    exact initial weights (per-tensor sums of the reference's seeded init, tests/golden/vitl_autocast.pt):
+    the premise of the bf16-autocast comparison in test_gpu_model.py."""
+    from vjepa2_amd.vision_transformer import vit_large
+
+    d = torch.load(os.path.join(GOLD, "vitl_autocast.pt"), weights_only=True)
+    torch.manual_seed(d["seed"])
+    enc = vit_large(img_size=64, num_frames=16, tubelet_size=2, use_rope=True, uniform_power=True, use_sdpa=True)
+    sd = enc.state_dict()
+    assert set(sd) == set(d["param_sums"])
+    for k, v in sd.items():
+        assert abs(float(v.double().sum()) - d["param_sums"][k]) <= 1e-9 * (1 + abs(d["param_sums"][k])), k

@@ -72,7 +72,10 @@ class FlatArena:
             p.data = view
             if grads:
                 p.grad = self.grad[o:o + n].view(p.shape)
+                p._vj_arena = self
+                p._vj_gepoch = 0
             p._vj_bf16 = self.bf16[o:o + n].view(p.shape)
+        self.epoch = 0  # gradient epoch: bumped by zero_grad(); a param's grad is current iff its epoch matches
         self.sync_bf16()
 
     def sync_bf16(self):
@@ -92,8 +95,41 @@ class FlatArena:
         return self.offsets[i], self.offsets[j - 1] + _padded(self.params[j - 1].numel())
 
     def zero_grad(self):
-        if self.grad is not None:
+        """Zero the gradients, lazily for the weights that a weight-gradient GEMM overwrites on its
+        first write of a step (functions.wgrad_buf marks them): those keep their old values until
+        then (no fill pass over ~1.3 GB of ViT-L gradients, and the GEMM epilogue does not read them
+        back). Every other gradient is zeroed here, in contiguous runs."""
+        if self.grad is None:
+            return
+        self.epoch += 1
+        ow = [getattr(p, "_vj_ow", False) for p in self.params]
+        if not any(ow):
             self.grad.zero_()
+            for p in self.params:
+                p._vj_gepoch = self.epoch
+            return
+        i, n = 0, len(self.params)
+        while i < n:
+            if ow[i]:
+                i += 1
+                continue
+            j = i
+            while j < n and not ow[j]:
+                self.params[j]._vj_gepoch = self.epoch
+                j += 1
+            lo, hi = self.span(i, j)
+            self.grad[lo:hi].zero_()
+            i = j
+
+    def finalize_grads(self):
+        """Zero the lazily zeroed gradients nothing wrote this step (their values are a previous
+        step's): after the backward, before anything reads the whole gradient arena."""
+        if self.grad is None:
+            return
+        for p in self.params:
+            if p._vj_gepoch != self.epoch:
+                p.grad.zero_()
+                p._vj_gepoch = self.epoch
 
 
 class FusedAdamW:
@@ -148,6 +184,8 @@ class FusedAdamW:
 
     def step(self, grad_scale=1.0, found_inf=None, exclude=()):
         self._resolve()
+        for a in self.arenas:
+            a.finalize_grads()
         ex = {id(p) for p in exclude}
         advanced = []
         for i, (g, a) in enumerate(zip(self.param_groups, self.arenas)):
@@ -183,6 +221,8 @@ class FusedAdamW:
 
     def check_finite(self):
         """GradScaler inf/NaN detection over every gradient arena -> device flag (no host sync)."""
+        for a in self.arenas:
+            a.finalize_grads()
         if self.found_inf is None:
             self.found_inf = torch.zeros(1, dtype=torch.int32, device=self.arenas[0].data.device)
         self.found_inf.zero_()

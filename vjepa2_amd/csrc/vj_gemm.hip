@@ -272,6 +272,9 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
                                    void* stream) {
   if (M == 0 || N == 0) return VJ_OK;
   VJ_CHECK_ARG(M > 0 && N > 0 && K > 0, "vj_gemm_bf16: bad dims M=%d N=%d K=%d", M, N, K);
+  VJ_CHECK_ARG(epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID || epi == EPI_GELU || epi == EPI_GELU_BWD ||
+                   epi == EPI_BF16_RESID,
+               "vj_gemm_bf16: epilogue %d is not a public epilogue (0-4, 7; include/vjepa_hip.h)", epi);
   VJ_CHECK_ARG(A && B, "vj_gemm_bf16: null operand");
   VJ_CHECK_ARG(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0, "vj_gemm_bf16: operands must be 16-B aligned");
   VJ_CHECK_ARG(lda % 8 == 0 && ldb % 8 == 0, "vj_gemm_bf16: lda/ldb must be multiples of 8 (lda=%ld ldb=%ld)", lda, ldb);

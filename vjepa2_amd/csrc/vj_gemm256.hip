@@ -888,7 +888,7 @@ int launch256(int epi, const G256& g, hipStream_t st) {
 
 }  // namespace
 
-bool vj_gemm_pp_enabled();
+bool vj_gemm_pp_enabled(int epi);
 int vj_gemm_pp_dispatch(int M, int N, int K, const void* A, long lda, const void* B, long ldb, int epi,
                         const float* bias, const void* aux, long ldaux, void* C, long ldc, void* C2, long ldc2,
                         hipStream_t st, const void* rope, int group, int grid);
@@ -903,7 +903,7 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
   if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
     return VJ_ERR_UNSUPPORTED;
   // K-major A and B: the ping-pong kernel (vj_gemm_pp.hip) when it takes the shape
-  if (a_kmajor && b_kmajor && vj_gemm_pp_enabled()) {
+  if (a_kmajor && b_kmajor && vj_gemm_pp_enabled(epi)) {
     const int tm = vj_cdiv(M, 256), tn = vj_cdiv(N, 128);
     const int rc = vj_gemm_pp_dispatch(M, N, K, A, lda, B, ldb, epi, bias, aux, ldaux, C, ldc, C2, ldc2, st, rope,
                                        tile_group(tm, tn), grid256((long)tm * tn));

@@ -191,6 +191,26 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
         acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * 4 + i][j], 0, 0, 0);
   };
 
+  // single-fragment reads and one phase = 16 MFMAs on (M-half mh) x (4 n-tiles), each followed by
+  // side(q) (reads / DMA for later phases), the order pinned by scheduling barriers
+  auto rdA1 = [&](bf16x8 (&X)[4], int i, int slot, int mh, int ks) {
+    const uint32_t base = lds0 + slot * STAGE + wr * 128 * 128;
+    X[i] = *(const LDS_AS bf16x8*)((const LDS_AS char*)(uintptr_t)(base + loff[ks]) + (mh * 4 + i) * 16 * 128);
+  };
+  auto rdB1 = [&](bf16x8 (&Y)[NTN], int j, int slot, int ks) {
+    const uint32_t base = lds0 + slot * STAGE + A_BYTES + wc * WN * 128;
+    Y[j] = *(const LDS_AS bf16x8*)((const LDS_AS char*)(uintptr_t)(base + loff[ks]) + j * 16 * 128);
+  };
+  auto phase = [&](const bf16x8 (&X)[4], int mh, const bf16x8 (&Y)[NTN], auto&& side) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      acc[mh * 4 + (q >> 2)][q & 3] =
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[q >> 2], Y[q & 3], acc[mh * 4 + (q >> 2)][q & 3], 0, 0, 0);
+      side(q);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   // ---- the K-loop of one tile (nk barriers); u0 = its first K-tile in the pipeline
   // The K-loop of tile p (first K-tile u0 of the pipeline). After barrier b = u0 + t it DMAs K-tile
   // b + NST: K-tile t + NST of this tile, else K-tile t + NST - nk of tile p + 1 (nk >= NST), whose
@@ -212,19 +232,14 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
     int sl = u0 % NST;  // slot of K-tile u0 + t
     for (int t = 0; t < nk; ++t) {
       const int sn = sl + 1 == NST ? 0 : sl + 1;
-      rdA(Ab, sl, 1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(Aa, 0, Ba);
-      __builtin_amdgcn_sched_barrier(0);
-      rdA(Aa, sl, 0, 1);
-      rdB(Bb, sl, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(Ab, 1, Ba);
-      __builtin_amdgcn_sched_barrier(0);
-      rdA(Ab, sl, 1, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(Aa, 0, Bb);
-      __builtin_amdgcn_sched_barrier(0);
+      // phases 0-2: 16 MFMAs each with the next phase's fragment reads issued one per MFMA gap
+      // (a lone wave per SIMD drives the matrix pipe here: nothing may bunch in front of the MFMAs)
+      phase(Aa, 0, Ba, [&](int q) { if (q < 4) rdA1(Ab, q, sl, 1, 0); });
+      phase(Ab, 1, Ba, [&](int q) {
+        if (q < 4) rdA1(Aa, q, sl, 0, 1);
+        else if (q < 8) rdB1(Bb, q - 4, sl, 1);
+      });
+      phase(Aa, 0, Bb, [&](int q) { if (q < 4) rdA1(Ab, q, sl, 1, 1); });
       // Retire K-tile b + 1 = u0 + t + 1 and this wave's reads of K-tile b: every K-tile issues
       // exactly DMA_PIECES pieces per wave (past the last K-tile of the block they are dummies into
       // the freed slot), so "all but the youngest DMA_PIECES" leaves only K-tile b + 2 in flight.
@@ -235,12 +250,9 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
       asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      // the next K-tile's phase-0 fragments (past the tile's last K-tile: harmless reads of the
-      // next tile's data, overwritten before use), then phase 3's 16 MFMAs with the 12 LDS-DMA
-      // pieces of K-tile b + NST (into slot sl, just freed) issued one per MFMA gap
-      rdA(Aa, sn, 0, 0);
-      rdB(Ba, sn, 0);
-      __builtin_amdgcn_sched_barrier(0);
+      // phase 3 (the K-tile's last 16 MFMAs) with the next K-tile's phase-0 fragments (past the
+      // tile's last K-tile: harmless reads of the next tile's data, overwritten before use) and the
+      // 12 LDS-DMA pieces of K-tile b + NST (into slot sl, just freed) issued in its MFMA gaps
       {
         const int td = t + NST;
         const bool own = td < nk;
@@ -248,17 +260,15 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
         const int kb = (own ? td : td - nk) * BK * 2;
         const uint32_t kill = own ? 0u : killN;
         LDS_AS char* st = smem + sl * STAGE;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          acc[4 + (q >> 2)][q & 3] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ab[q >> 2], Bb[q & 3], acc[4 + (q >> 2)][q & 3], 0, 0, 0);
+        phase(Ab, 1, Bb, [&](int q) {
+          if (q < 4) rdA1(Aa, q, sn, 0, 0);
+          else if (q < 8) rdB1(Ba, q - 4, sn, 0);
           if (q < 8)  // A rows (w4 * 8 + q) * 8 .. + 7: piece q = base + 16 (q >> 1) rows
             dma16s(ra, st + (w4 * 8 + q) * 1024, (aoff[q & 1] + (uint32_t)((q >> 1) * 16 * g.lda * 2)) | kill, kb);
           else if (q < 12)  // B LDS rows (w4 * 4 + i) * 8 .. + 7: global rows of piece i & 1 + (i >> 1)
             dma16s(rb, st + A_BYTES + (w4 * 4 + (q - 8)) * 1024,
                    (boff[q & 1] + (uint32_t)(((q - 8) >> 1) * g.ldb * 2)) | kill, kb);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+        });
       }
       sl = sn;
     }
@@ -450,11 +460,16 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
 
 }  // namespace
 
-// VJ_GEMM_PP=1 routes the K-major GEMMs here (off by default until it beats k_gemm256 on the
-// train-step shapes: tools/bench_kernels.py @VJ_GEMM_PP=0 @VJ_GEMM_PP=1)
-bool vj_gemm_pp_enabled() {
+// Which K-major GEMMs come here: VJ_GEMM_PP=0 none, =1 all, unset: the epilogues in the bit mask
+// VJ_GEMM_PP_EPIS (default: the QKV + RoPE epilogue, the shape where it measured faster than
+// k_gemm256; tools/bench_kernels.py @VJ_GEMM_PP=0 @VJ_GEMM_PP=1)
+bool vj_gemm_pp_enabled(int epi) {
   const char* e = getenv("VJ_GEMM_PP");
-  return e && e[0] == '1';
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  const char* m = getenv("VJ_GEMM_PP_EPIS");
+  const long mask = m ? strtol(m, nullptr, 0) : (1L << EPI_ROPE);
+  return (mask >> epi) & 1;
 }
 
 // Called by vj_gemm256_dispatch for K-major A and B; VJ_ERR_UNSUPPORTED when the shape is not one

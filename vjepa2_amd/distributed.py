@@ -89,6 +89,7 @@ class GradReducer:
         self.reset()
 
     def reset(self):
+        self.armed = True  # False during the backward of all but the last frames-per-clip group
         for b in self.buckets + self.tail:
             b.pending = {id(p) for p in b.params}
             b.work = None
@@ -99,6 +100,8 @@ class GradReducer:
 
     def mark_ready(self, module):
         """Hook called when `module`'s backward has finished writing its parameter gradients."""
+        if not self.armed:
+            return
         for p in module.parameters():
             i = self.owner.get(id(p))
             if i is not None:

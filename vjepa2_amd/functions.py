@@ -69,9 +69,35 @@ def weight_fp8(p):
 
 
 def grad_buf(p):
+    """p.grad for an accumulating (+=) write. Gradients in a lazily zeroed arena (FlatArena.zero_grad
+    skips the weights the weight-gradient GEMMs overwrite) are zeroed here on their first touch of
+    the step if that touch is not an overwrite."""
     if p.grad is None:
         p.grad = torch.zeros_like(p)
+    a = getattr(p, "_vj_arena", None)
+    if a is not None and p._vj_gepoch != a.epoch:
+        p.grad.zero_()
+        p._vj_gepoch = a.epoch
     return p.grad
+
+
+def wgrad_buf(p):
+    """(p.grad, accumulate) for a weight-gradient GEMM: the first write of the step overwrites
+    (EPI_F32: no zero fill of the gradient, no read of it in the epilogue), later writes add."""
+    a = getattr(p, "_vj_arena", None)
+    if a is None or p.grad is None:
+        return grad_buf(p), True
+    p._vj_ow = True
+    if p._vj_gepoch != a.epoch:
+        p._vj_gepoch = a.epoch
+        return p.grad, False
+    return p.grad, True
+
+
+def wgrad(dy, x, w, shape=None):
+    """dW (+)= dY^T X into w's gradient (nn.Linear / Conv3d-as-GEMM weight gradient)."""
+    buf, acc = wgrad_buf(w)
+    ops.linear_wgrad(dy, x, buf if shape is None else buf.view(*shape), accumulate=acc)
 
 
 _ROPE_TABLES = {}
@@ -234,23 +260,23 @@ def block_backward(dxo, blk, lay, saved):
     dxo_b = twin[0] if twin is not None and twin[1] == dxo._version else ops.cast_bf16(dxo)  # unless changed since
     # MLP
     dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
-    ops.linear_wgrad(dxo_b, act, grad_buf(mlp.fc2.weight))  # fc2 bias grad: fused into LN2 backward
+    wgrad(dxo_b, act, mlp.fc2.weight)  # fc2 bias grad: fused into LN2 backward
     dln2 = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
-    ops.linear_wgrad(dpre, ln2, grad_buf(mlp.fc1.weight))
+    wgrad(dpre, ln2, mlp.fc1.weight)
     _bias_grad(mlp.fc1, dpre)
     gw, gb = _ln_grads(blk.norm2)
     dxm, dxm_b = ops.layernorm_bwd(dln2, x_mid, m2, r2, blk.norm2.weight, dres_in=dxo, dweight=gw, dbias=gb,
                                    want_bf16=True, sum_in=_bias_buf(mlp.fc2), sum_out=_bias_buf(attn.proj))
     # attention (proj bias grad = column sums of dxm, produced above)
     do = ops.linear_dgrad(dxm_b, weight_bf16(attn.proj.weight), wt=weight_bf16_t(attn.proj.weight))
-    ops.linear_wgrad(dxm_b, o, grad_buf(attn.proj.weight))
+    wgrad(dxm_b, o, attn.proj.weight)
     rope = None
     if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
     dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk)
     dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
-    ops.linear_wgrad(dqkv, ln1, grad_buf(attn.qkv.weight))
+    wgrad(dqkv, ln1, attn.qkv.weight)
     _bias_grad(attn.qkv, dqkv)
     gw, gb = _ln_grads(blk.norm1)
     dxi, dxi_b = ops.layernorm_bwd(dln1, x, m1, r1, blk.norm1.weight, dres_in=dxm, dweight=gw, dbias=gb,
@@ -321,7 +347,7 @@ def attn_module_backward(dy, attn, lay, saved):
     hd = x.shape[1] // H
     dy_b = ops.cast_bf16(dy)
     do = ops.linear_dgrad(dy_b, weight_bf16(attn.proj.weight), wt=weight_bf16_t(attn.proj.weight))
-    ops.linear_wgrad(dy_b, o, grad_buf(attn.proj.weight))
+    wgrad(dy_b, o, attn.proj.weight)
     _bias_grad(attn.proj, dy)
     rope = None
     if attn.use_rope:
@@ -329,7 +355,7 @@ def attn_module_backward(dy, attn, lay, saved):
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
     dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk)
     dx = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
-    ops.linear_wgrad(dqkv, x, grad_buf(attn.qkv.weight))
+    wgrad(dqkv, x, attn.qkv.weight)
     _bias_grad(attn.qkv, dqkv)
     return dx
 
@@ -347,10 +373,10 @@ def mlp_module_backward(dy, mlp, saved):
     x, dgelu, act = saved
     dy_b = ops.cast_bf16(dy)
     dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
-    ops.linear_wgrad(dy_b, act, grad_buf(mlp.fc2.weight))
+    wgrad(dy_b, act, mlp.fc2.weight)
     _bias_grad(mlp.fc2, dy)
     dx = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
-    ops.linear_wgrad(dpre, x, grad_buf(mlp.fc1.weight))
+    wgrad(dpre, x, mlp.fc1.weight)
     _bias_grad(mlp.fc1, dpre)
     return dx
 
@@ -428,7 +454,7 @@ class _PatchEmbedFn(torch.autograd.Function):
         proj = ctx.pe.proj
         D = proj.weight.shape[0]
         dx = dx.contiguous()
-        ops.linear_wgrad(ops.cast_bf16(dx), ctx.cols, grad_buf(proj.weight).view(D, -1))
+        wgrad(ops.cast_bf16(dx), ctx.cols, proj.weight, (D, -1))
         _bias_grad(proj, dx)
         ctx.cols = None
         _fire_hook(ctx.pe)
@@ -489,7 +515,7 @@ class _LinearFn(torch.autograd.Function):
         w = lin.weight
         wt = weight_bf16_t(w) if w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 else None  # else padded in linear_dgrad
         dx = ops.linear_dgrad(dy_b, weight_bf16(lin.weight), wt=wt)
-        ops.linear_wgrad(dy_b, ctx.x, grad_buf(lin.weight))
+        wgrad(dy_b, ctx.x, lin.weight)
         _bias_grad(lin, dy)
         ctx.x = None
         _fire_hook(lin)

@@ -9,8 +9,9 @@ import torch
 from ._lib import call, int_array
 
 EPI_BF16, EPI_F32, EPI_F32_RESID, EPI_GELU, EPI_GELU_BWD = 0, 1, 2, 3, 4
+EPI_ROPE, EPI_PARTIAL = 5, 6  # internal to the library (vj_qkv_rope_gemm / split-K slabs): not for vj_gemm_bf16
 EPI_BF16_RESID = 7  # bf16 residual in, bf16 out (no-grad target encoder: the reference's autocast precision)
-EPI_NAMES = ["EPI_BF16", "EPI_F32", "EPI_F32_RESID", "EPI_GELU", "EPI_GELU_BWD", "EPI_5", "EPI_6", "EPI_BF16_RESID"]
+EPI_NAMES = ["EPI_BF16", "EPI_F32", "EPI_F32_RESID", "EPI_GELU", "EPI_GELU_BWD", "EPI_ROPE", "EPI_PARTIAL", "EPI_BF16_RESID"]
 BF16 = torch.bfloat16
 F32 = torch.float32
 
@@ -202,23 +203,33 @@ def _pad_rows(t):
     return out
 
 
-def linear_wgrad(dy, x, dw):
-    """dW[N,K] += dY^T X  (f32 accumulate into dw)."""
+def linear_wgrad(dy, x, dw, accumulate=True):
+    """dW[N,K] += dY^T X  (f32 accumulate into dw); accumulate=False: dW = dY^T X (overwrite)."""
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dw.shape == (N, K) and dw.dtype == F32
     if N % 8:  # dY^T is the MN-major A operand: its contiguous dim N must be a multiple of 8
         tmp = torch.zeros((N + 7) // 8 * 8, K, dtype=F32, device=dw.device)
         linear_wgrad(_pad_cols(dy), x, tmp)
-        dw += tmp[:N]
+        if accumulate:
+            dw += tmp[:N]
+        else:
+            dw.copy_(tmp[:N])
         return dw
     if K % 8:  # X is the MN-major B operand: same for its width K
         tmp = torch.zeros(N, (K + 7) // 8 * 8, dtype=F32, device=dw.device)
         linear_wgrad(dy, _pad_cols(x), tmp)
-        dw += tmp[:, :K]
+        if accumulate:
+            dw += tmp[:, :K]
+        else:
+            dw.copy_(tmp[:, :K])
         return dw
-    gemm(N, K, M, dy, _rowmajor(dy, "dy"), False, x, _rowmajor(x, "x"), False, EPI_F32_RESID, out=dw,
-         ldc=dw.stride(0), aux=dw, ldaux=dw.stride(0), splitk=wgrad_splitk(N, K, M))
+    if accumulate:
+        gemm(N, K, M, dy, _rowmajor(dy, "dy"), False, x, _rowmajor(x, "x"), False, EPI_F32_RESID, out=dw,
+             ldc=dw.stride(0), aux=dw, ldaux=dw.stride(0), splitk=wgrad_splitk(N, K, M))
+    else:
+        gemm(N, K, M, dy, _rowmajor(dy, "dy"), False, x, _rowmajor(x, "x"), False, EPI_F32, out=dw,
+             ldc=dw.stride(0), splitk=wgrad_splitk(N, K, M))
     return dw
 
 

@@ -193,23 +193,35 @@ class JEPATrainer:
 
     def compute_grads(self, clips, masks_enc, masks_pred):
         """Forward + backward (train.py:414-445): gradients land in the arenas, all-reduced (summed)
-        across ranks when world > 1."""
-        if len(clips) != 1:
-            raise NotImplementedError("one frames-per-clip group per step on the fused path "
-                                      "(configs with dataset_fpcs all equal produce exactly one)")
-        loss, zp, dz = self.forward_loss(clips[0], masks_enc[0], masks_pred[0], mask_index=0,
-                                         npairs=len(masks_enc[0]))
-        zp.backward(dz)
+        across ranks when world > 1. Several frames-per-clip groups (one entry per group in clips /
+        masks_*) run one after the other, group i's predictor with mask token i (wrappers.py:20-43,
+        mask_index = i); the loss is the mean over every (group, mask) pair (train.py:425-435), so
+        each group's loss and dL/dz carry 1 / (all pairs). The gradient all-reduce is armed only for
+        the last group's backward: a parameter's gradient is complete only after every group's."""
+        G = len(clips)
+        if not (G == len(masks_enc) == len(masks_pred)) or G == 0:
+            raise ValueError("clips / masks_enc / masks_pred: one entry per frames-per-clip group")
+        npairs = sum(len(m) for m in masks_enc)
+        total = None
+        for i in range(G):
+            if self.reducer is not None:
+                self.reducer.armed = i == G - 1
+            loss, zp, dz = self.forward_loss(clips[i], masks_enc[i], masks_pred[i], mask_index=i, npairs=npairs)
+            zp.backward(dz)
+            total = loss if total is None else total + loss
+        self._groups = G
+        for a in self.opt.arenas:  # lazily zeroed gradients nothing wrote (before the tail buckets)
+            a.finalize_grads()
         if self.reducer is not None:
             self.reducer.finish()
-        return loss
+        return total
 
     def apply_update(self, momentum):
         """GradScaler inf-check + AdamW (train.py:446-454) + EMA (train.py:456-465). The 1/world
         average of the summed gradients is folded into AdamW. Mask tokens other than the one this
         step used have grad None in the reference, so they take no step (no decay either)."""
         found = self.opt.check_finite() if self.mixed_precision else None
-        used = {0 % max(1, len(self.mask_tokens))}
+        used = {i % max(1, len(self.mask_tokens)) for i in range(getattr(self, "_groups", 1))}
         unused = [t for i, t in enumerate(self.mask_tokens) if i not in used]
         self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused)
         self.opt.zero_grad()

@@ -7,6 +7,7 @@ Index/byte kernels (gather/scatter/fill/index build) must be bit-exact.
 """
 
 import math
+import os
 
 import pytest
 import torch
@@ -180,7 +181,7 @@ def test_gemm_persistent_walk(knobs, monkeypatch):
         test_gemm_epilogues(M, N)
     test_gemm_splitk(2, (520, 392, 3000))
     test_gemm_splitk(0, (512, 256, 4100))
-    test_fused_rope_paths(1500, 64, 2)
+    test_fused_rope_paths(1500, 64, 2, monkeypatch)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -203,7 +204,10 @@ def _attn_ref(q, k, v, groups, scale):
                                          # vit_huge / vit_giant head dims (padded to 96 inside)
                                          (80, 2, [(2, 150), (1, 33)]), (88, 2, [(1, 200), (3, 31)]),
                                          # long sequences: ViT-L 16x256^2 (2048), ViT-g 16x384^2 (4608)
-                                         (64, 2, [(1, 2048), (1, 4608)]), (32, 2, [(1, 4608), (1, 1504)])])
+                                         (64, 2, [(1, 2048), (1, 4608)]), (32, 2, [(1, 4608), (1, 1504)]),
+                                         # ViT-g 64x256^2: predictor n = 6013 (hd 32), context K = 2398
+                                         # and the full 8192-token target sequence (hd 64)
+                                         (32, 2, [(1, 6013)]), (64, 2, [(1, 2398), (1, 8192)])])
 def test_attention_fwd_bwd(hd, H, groups):
     from vjepa2_amd import ops
 
@@ -315,6 +319,14 @@ def test_layernorm(D):
     _close(y, yr, 1e-4, 1e-4, "ln fwd")
     yb, _, _ = ops.layernorm_fwd(x, w, b, 1e-6)
     _close(yb, yr, 1e-3, 8e-3, "ln fwd bf16")
+    # bf16 input rows (the no-grad target encoder's bf16 residual stream), f32 and bf16 outputs
+    xb = x.bfloat16()
+    ref_b = torch.nn.functional.layer_norm(xb.float(), (D,), w, b, 1e-6)
+    y32b, mb, rb = ops.layernorm_fwd(xb, w, b, 1e-6, out_dtype=torch.float32)
+    _close(y32b, ref_b, 1e-4, 1e-4, "ln fwd (bf16 x)")
+    _close(mb, xb.float().mean(1), 1e-5, 1e-5, "ln fwd mean (bf16 x)")
+    y16b, _, _ = ops.layernorm_fwd(xb, w, b, 1e-6)
+    _close(y16b, ref_b, 1e-3, 8e-3, "ln fwd bf16 (bf16 x)")
     dy = torch.randn(M, D, generator=g).to(DEV).bfloat16()
     yr.backward(dy.float())
     dres_in = torch.randn(M, D, generator=g).to(DEV)
@@ -397,11 +409,15 @@ def test_fused_rope_paths(M, hd, H, monkeypatch):
     b = torch.randn(3 * D, generator=g).to(DEV)
     fused = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
     if M >= 1024:  # ping-pong kernel == one-tile-per-workgroup kernel, bitwise
+        prev = os.environ.get("VJ_GEMM_PP")
         for pp in ("1", "0"):
             monkeypatch.setenv("VJ_GEMM_PP", pp)
             other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
             assert torch.equal(fused, other), f"qkv_rope: VJ_GEMM_PP={pp} differs from the default kernel"
-        monkeypatch.delenv("VJ_GEMM_PP")
+        if prev is None:
+            monkeypatch.delenv("VJ_GEMM_PP")
+        else:
+            monkeypatch.setenv("VJ_GEMM_PP", prev)
     # expected: our own f32 GEMM (same accumulation), RoPE in fp32 by the oracle
     y32 = ops.linear_fwd(x, w, b, ops.EPI_F32).cpu()
     idl = ids.cpu().long()[None]

@@ -80,7 +80,10 @@ def test_two_fpc_groups_vs_oracle():
     [8, 4]): the MaskCollator yields one (clips, masks) entry per group; the reference runs the
     wrappers' per-group loop (wrappers.py:20-43, predictor mask_index = group) and averages the loss
     over every (group, mask) pair (train.py:425-435). HIP fused step vs the CPU oracle's
-    step_groups on the same weights / clips / masks: loss within 1e-2 relative, AdamW update signs."""
+    loss_groups on the same weights / clips / masks: loss within 1e-2 relative, every parameter
+    gradient within rel-L1 6e-2 of fp32 autograd (bf16 operands; a single group measures 3.4e-2 on
+    this tiny config), unused mask tokens untouched. The 4-frame group has fewer tokens per clip than
+    the model's 8-frame maximum: its loss rows index the target by the clip's own token count."""
     from vjepa2_amd.masks import MaskCollator
     from vjepa2_amd.train import JEPATrainer, init_opt, init_video_model
 
@@ -110,18 +113,38 @@ def test_two_fpc_groups_vs_oracle():
     gen = torch.Generator().manual_seed(1)
     clips = [torch.randn(B, 3, T, S, S, generator=gen) for T in (8, 4)]
     tok0 = [t.detach().cpu().clone() for t in tr.mask_tokens]
-    loss = tr.train_step([c.to(dev) for c in clips], [[m.to(dev) for m in g[1]] for g in groups],
-                         [[m.to(dev) for m in g[2]] for g in groups], 0.99925).item()
+    loss = tr.compute_grads([c.to(dev) for c in clips], [[m.to(dev) for m in g[1]] for g in groups],
+                            [[m.to(dev) for m in g[2]] for g in groups]).item()
+    torch.cuda.synchronize()
+    got = {("enc", k): p.grad.detach().cpu().clone() for k, p in enc.backbone.named_parameters()}
+    got.update({("pred", k): p.grad.detach().cpu().clone() for k, p in pred.backbone.named_parameters()
+                if p.grad is not None})
+    tr.apply_update(0.99925)
     ref = orc.OracleTrainer(enc_sd, pred_sd, dict(patch_size=16, tubelet_size=2, num_heads=6, depth=12, use_rope=True),
                             dict(num_heads=12, depth=2, use_rope=True, grid_size=S // 16, num_mask_tokens=4,
                                  num_patches=4 * (S // 16) ** 2))
-    ref_loss = ref.step_groups([(c, g[1], g[2]) for c, g in zip(clips, groups)], 1e-4, 0.04, 0.99925)
+    ref_loss_t = ref.loss_groups([(c, g[1], g[2]) for c, g in zip(clips, groups)])
+    ref_loss_t.backward()
+    ref_loss = ref_loss_t.item()
     rel = abs(loss - ref_loss) / abs(ref_loss)
-    w = enc.backbone.blocks[0].attn.qkv.weight.detach().cpu()
-    w0 = enc_sd["blocks.0.attn.qkv.weight"]
-    agree = (torch.sign(w - w0) == torch.sign(ref.enc["blocks.0.attn.qkv.weight"].detach() - w0)).float().mean().item()
-    print(f"2 fpc groups: loss {loss:.6f} vs oracle {ref_loss:.6f} (rel {rel:.2e}), update sign agreement {agree:.4f}")
-    assert rel < 1e-2 and agree > 0.9
+    rep = [f"2 fpc groups: loss {loss:.6f} vs oracle {ref_loss:.6f} (rel {rel:.2e})"]
+    assert rel < 1e-2, rep
+    # gradients (before the optimizer) vs fp32 autograd of the oracle, bf16-operand envelope
+    worst = 0.0
+    for (which, k), gk in got.items():
+        rp = (ref.enc if which == "enc" else ref.pred)[k]
+        if rp.grad is None:
+            assert gk.abs().max() == 0, f"{which}.{k}: gradient where the reference has none"
+            continue
+        e = ((gk - rp.grad).abs().sum() / rp.grad.abs().sum().clamp_min(1e-30)).item()
+        worst = max(worst, e)
+        if e > 4e-2:
+            rep.append(f"{which}.{k}: rel_l1 {e:.3e}")
+    rep.append(f"worst gradient rel_l1 {worst:.3e}")
+    print("\n".join(rep))
+    # bf16 operands on this tiny config (D = 384, <= 64 tokens per clip): one group alone measures a
+    # worst gradient rel-L1 of 3.4e-2 against the same oracle (tools/debug_groups.py)
+    assert worst < 6e-2, "\n".join(rep)
     # mask tokens 0 and 1 (one per group) took a step; tokens 2 and 3 (unused) did not move
     for i, t in enumerate(tr.mask_tokens):
         moved = not torch.equal(t.detach().cpu(), tok0[i])

@@ -161,6 +161,29 @@ def ln_bwd_case(lib, M, D, acc, dev, stream):
     return run, byt * 1e3
 
 
+# (name, M, D, x bf16): LayerNorm forward of the block's norm1 / norm2 (bf16 out + mean / rstd); TB/s
+LNF = [("ln fwd tgt bf16", 49152, 1024, True), ("ln fwd ctx f32", 15432, 1024, False),
+       ("ln fwd pred f32", 73104, 384, False)]
+
+
+def ln_fwd_case(lib, M, D, xbf, dev, stream):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(M, D, generator=g).to(dev)
+    if xbf:
+        x = x.bfloat16()
+    y = torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    gamma = torch.rand(D, generator=g).to(dev)
+    beta = torch.rand(D, generator=g).to(dev)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def run():
+        rc = lib.vj_layernorm_fwd(M, D, p(x), int(xbf), D, p(gamma), p(beta), 1e-6, p(y), 0, D, p(mean), p(rstd), stream)
+        assert rc == 0, rc
+    return run, M * D * ((2 if xbf else 4) + 2) * 1e3
+
+
 def time_fn(fn, iters=10):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
@@ -210,6 +233,10 @@ def main():
         if only and only not in name:
             continue
         cases.append((name, [attn_case(lib, hd, H, groups, dev, stream, bwd) for lib in libs]))
+    for name, M, D, xbf in LNF:
+        if only and only not in name:
+            continue
+        cases.append((name, [ln_fwd_case(lib, M, D, xbf, dev, stream) for lib in libs]))
     for name, M, D, acc in LNB:
         if only and only not in name:
             continue

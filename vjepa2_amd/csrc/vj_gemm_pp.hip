@@ -461,14 +461,17 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
 }  // namespace
 
 // Which K-major GEMMs come here: VJ_GEMM_PP=0 none, =1 all, unset: the epilogues in the bit mask
-// VJ_GEMM_PP_EPIS (default: the QKV + RoPE epilogue, the shape where it measured faster than
-// k_gemm256; tools/bench_kernels.py @VJ_GEMM_PP=0 @VJ_GEMM_PP=1)
+// VJ_GEMM_PP_EPIS (default none). Measured (tools/bench_kernels.py @VJ_GEMM_PP=0 @VJ_GEMM_PP=1,
+// MI355X): faster only on the context / predictor QKV + RoPE shapes (76 vs 84-87 us), slower on the
+// target QKV and every other epilogue (the lone-wave K-loop runs at ~0.9 of the two-wave one and
+// the epilogues do not fully hide under it); the step measured 192.2 clips/s with the RoPE shapes
+// routed here vs 193.4 without (bench.py A/B in one call), so the default stays k_gemm256.
 bool vj_gemm_pp_enabled(int epi) {
   const char* e = getenv("VJ_GEMM_PP");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
   const char* m = getenv("VJ_GEMM_PP_EPIS");
-  const long mask = m ? strtol(m, nullptr, 0) : (1L << EPI_ROPE);
+  const long mask = m ? strtol(m, nullptr, 0) : 0L;
   return (mask >> epi) & 1;
 }
 

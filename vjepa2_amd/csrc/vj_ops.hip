@@ -135,6 +135,98 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
   }
 }
 
+// LayerNorm forward, persistent: each wave walks rows w, w + W, ... (W = waves in the grid) with the
+// next row's loads issued before the current row's reductions; every lane moves 16 B per access
+// (E = 8 bf16 or 4 f32 elements of x; the bf16 output row goes out as 16-B / 8-B stores), and the
+// affine parameters are loaded once per wave. Element map: vector i of lane l holds the E elements
+// (64 i + l) E ... Replaces k_ln_fwd for the bf16 / f32 outputs (the fp8 output keeps k_ln_fwd).
+template <bool XBF, bool YF32, int NV>
+__global__ __launch_bounds__(256) void k_ln_fwd2(int M, int D, const void* __restrict__ x, long ldx,
+                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                 float eps, void* __restrict__ y, long ldy, float* __restrict__ mean,
+                                                 float* __restrict__ rstd) {
+  constexpr int E = XBF ? 8 : 4;
+  const int lane = threadIdx.x & 63;
+  const long W = (long)gridDim.x * 4;
+  long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float g[NV][E], bb[NV][E], v[NV][E], vn[NV][E];
+  auto ok = [&](int i) { return (i * 64 + lane) * E < D; };
+  auto load = [&](long r, float (&dst)[NV][E]) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (!ok(i)) continue;
+      const long off = r * ldx + (i * 64 + lane) * E;
+      if constexpr (XBF) {
+        const uint4 u = *(const uint4*)((const bf16_t*)x + off);
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          dst[i][2 * k] = __builtin_bit_cast(float, w[k] << 16);
+          dst[i][2 * k + 1] = __builtin_bit_cast(float, w[k] & 0xffff0000u);
+        }
+      } else {
+        const float4 f = *(const float4*)((const float*)x + off);
+        dst[i][0] = f.x; dst[i][1] = f.y; dst[i][2] = f.z; dst[i][3] = f.w;
+      }
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+      const int c = (i * 64 + lane) * E + k;
+      g[i][k] = gamma && ok(i) ? gamma[c] : 1.f;
+      bb[i][k] = gamma && ok(i) ? beta[c] : 0.f;
+    }
+  load(row, v);
+  for (; row < M; row += W) {
+    if (row + W < M) load(row + W, vn);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if (ok(i))
+#pragma unroll
+        for (int k = 0; k < E; ++k) s += v[i][k];
+    const float mu = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if (ok(i))
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+          const float a = v[i][k] - mu;
+          q += a * a;
+        }
+    const float rs = rsqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (!ok(i)) continue;
+      float o[E];
+#pragma unroll
+      for (int k = 0; k < E; ++k) o[k] = (v[i][k] - mu) * rs * g[i][k] + bb[i][k];
+      const long off = row * ldy + (i * 64 + lane) * E;
+      if constexpr (YF32) {
+#pragma unroll
+        for (int k = 0; k < E; k += 4) *(float4*)((float*)y + off + k) = make_float4(o[k], o[k + 1], o[k + 2], o[k + 3]);
+      } else if constexpr (E == 8) {
+        *(uint4*)((bf16_t*)y + off) = make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]), pack_bf2(o[4], o[5]),
+                                                 pack_bf2(o[6], o[7]));
+      } else {
+        *(uint2*)((bf16_t*)y + off) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+      }
+    }
+    if (lane == 0) {
+      if (mean) mean[row] = mu;
+      if (rstd) rstd[row] = rs;
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int k = 0; k < E; ++k) v[i][k] = vn[i][k];
+  }
+}
+
 // Per-row fp8 quantisation of a [M, K] f32 / bf16 matrix (the fp8 target encoder's weights, one
 // scale per output channel): wave per row, two passes over the row (amax, then scaled e4m3 bytes).
 template <bool XBF>
@@ -244,6 +336,110 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
               const float4 v = *a;
               *a = make_float4(v.x + acc[k][i].x, v.y + acc[k][i].y, v.z + acc[k][i].z, v.w + acc[k][i].w);
             }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  for (int k = 0; k < nsum; ++k)
+    for (int c = threadIdx.x; c < D; c += 256) ws[((long)blockIdx.x * nsum + k) * D + c] = red[k][c];
+}
+
+// LayerNorm backward, 16-B accesses: lane l's vector i holds the 8 columns (64 i + l) * 8 .. + 7 of
+// every operand (dy bf16 16 B, x / dres_in / dres f32 2 x 16 B, dres bf16 16 B); dres_in is loaded
+// with x and dy, before the row's reductions. Same outputs and fixed-order partials as k_ln_bwd.
+template <bool ACC, int NV, bool SUMS>
+__global__ __launch_bounds__(256) void k_ln_bwd2(int M, int D, const bf16_t* __restrict__ dy, long lddy,
+                                                 const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+                                                 const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                 const float* __restrict__ dres_in, long ldri, float* __restrict__ dres,
+                                                 long ldr, bf16_t* __restrict__ dres_bf, long ldrb, float* __restrict__ ws,
+                                                 int nsum) {
+  constexpr int E = 8;
+  __shared__ float red[4][NV * 64 * E];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  auto ok = [&](int i) { return (i * 64 + lane) * E < D; };
+  constexpr int NS = SUMS ? 4 : 2;  // column partials kept: dgamma, dbeta (+ sums of dres_in, dres)
+  float acc[NS][NV][E];
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+#pragma unroll
+      for (int q = 0; q < NS; ++q) acc[q][i][k] = 0.f;
+  for (long row = (long)blockIdx.x * 4 + wave; row < M; row += (long)gridDim.x * 4) {
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NV][E], g[NV][E], ri[NV][E];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (!ok(i)) continue;
+      const int c = (i * 64 + lane) * E;
+      const float4 x0 = *(const float4*)(x + row * ldx + c), x1 = *(const float4*)(x + row * ldx + c + 4);
+      const uint4 u = *(const uint4*)(dy + row * lddy + c);
+      if constexpr (ACC) {
+        const float4 r0 = *(const float4*)(dres_in + row * ldri + c), r1 = *(const float4*)(dres_in + row * ldri + c + 4);
+        ri[i][0] = r0.x; ri[i][1] = r0.y; ri[i][2] = r0.z; ri[i][3] = r0.w;
+        ri[i][4] = r1.x; ri[i][5] = r1.y; ri[i][6] = r1.z; ri[i][7] = r1.w;
+      }
+      const float xv[E] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      float gm[E];  // gamma re-read per row (cache-resident) rather than held in 16 VGPRs
+      if (gamma) {
+        const float4 g0 = *(const float4*)(gamma + c), g1 = *(const float4*)(gamma + c + 4);
+        gm[0] = g0.x; gm[1] = g0.y; gm[2] = g0.z; gm[3] = g0.w; gm[4] = g1.x; gm[5] = g1.y; gm[6] = g1.z; gm[7] = g1.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < E; ++k) gm[k] = 1.f;
+      }
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < E; ++k) {
+        const float d = __builtin_bit_cast(float, (k & 1) ? (w[k >> 1] & 0xffff0000u) : (w[k >> 1] << 16));
+        xh[i][k] = (xv[k] - mu) * rs;
+        acc[1][i][k] += d;
+        acc[0][i][k] += d * xh[i][k];
+        g[i][k] = d * gm[k];
+        s1 += g[i][k];
+        s2 += g[i][k] * xh[i][k];
+      }
+    }
+    const float m1 = wave_sum(s1) / D, m2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (!ok(i)) continue;
+      const int c = (i * 64 + lane) * E;
+      float dx[E];
+#pragma unroll
+      for (int k = 0; k < E; ++k) {
+        dx[k] = rs * (g[i][k] - m1 - xh[i][k] * m2);
+        if constexpr (ACC) {
+          if constexpr (SUMS) acc[2][i][k] += ri[i][k];
+          dx[k] += ri[i][k];
+        }
+        if constexpr (SUMS) acc[3][i][k] += dx[k];
+      }
+      *(float4*)(dres + row * ldr + c) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+      *(float4*)(dres + row * ldr + c + 4) = make_float4(dx[4], dx[5], dx[6], dx[7]);
+      if (dres_bf)
+        *(uint4*)(dres_bf + row * ldrb + c) = make_uint4(pack_bf2(dx[0], dx[1]), pack_bf2(dx[2], dx[3]),
+                                                         pack_bf2(dx[4], dx[5]), pack_bf2(dx[6], dx[7]));
+    }
+  }
+  if (!ws) return;
+  // block reduction of the per-wave partials, waves added in fixed order (deterministic)
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        if (k >= nsum) break;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          if (!ok(i)) continue;
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            float* a = &red[k][(i * 64 + lane) * E + e];
+            *a = w == 0 ? acc[k][i][e] : *a + acc[k][i][e];
           }
         }
       }
@@ -815,11 +1011,34 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
   VJ_CHECK_ARG(D % 4 == 0 && D <= 64 * 4 * LN_MAXV, "vj_layernorm_fwd: D=%d must be %%4 and <= 2048", D);
   VJ_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "vj_layernorm_fwd: gamma/beta both or neither");
   VJ_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "vj_layernorm_fwd: strides must be %%4");
-  dim3 grid((M + 4 * LN_RPW - 1) / (4 * LN_RPW));
   hipStream_t st = (hipStream_t)stream;
-  const int nv = ln_nv(D);
+  // the per-16-row-block kernel: measured faster than the persistent 16-B-access k_ln_fwd2 on every
+  // train-step shape (tools/bench_kernels.py: 43 vs 47 us target, 19 vs 23 us context, 30 vs 36 us
+  // predictor); VJ_LN_FWD2=1 selects k_ln_fwd2
+  const char* e = getenv("VJ_LN_FWD2");
+  if (!(e && e[0] == '1')) {
+    dim3 grid((M + 4 * LN_RPW - 1) / (4 * LN_RPW));
+    const int nv = ln_nv(D);
 #define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, YF, NVV>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
 #define LNF_NV(XB, YF) switch (nv) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 4: LNF(XB, YF, 4); break; case 6: LNF(XB, YF, 6); break; default: LNF(XB, YF, 8); }
+    if (x_bf16 && y_f32) { LNF_NV(true, true) }
+    else if (x_bf16) { LNF_NV(true, false) }
+    else if (y_f32) { LNF_NV(false, true) }
+    else { LNF_NV(false, false) }
+#undef LNF_NV
+#undef LNF
+    VJ_LAUNCH_CHECK("vj_layernorm_fwd");
+    return VJ_OK;
+  }
+  // persistent: 4 blocks of 4 waves per CU (all resident at <= 128 VGPRs), fewer when M is small
+  const long want = ((long)M + 3) / 4;
+  const int grid = (int)(want < 256L * 4 ? want : 256L * 4);
+  const int E = x_bf16 ? 8 : 4;
+  const int nv = (D + 64 * E - 1) / (64 * E);  // 16-B vectors per lane
+  VJ_CHECK_ARG(D % E == 0 && ldx % E == 0 && nv <= 8, "vj_layernorm_fwd: D=%d, ldx must be %% %d", D, E);
+  VJ_CHECK_ARG(ldy % (y_f32 ? 4 : E) == 0, "vj_layernorm_fwd: ldy must be %% %d", y_f32 ? 4 : E);
+#define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd2<XB, YF, NVV>), dim3(grid), dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
+#define LNF_NV(XB, YF) switch (nv) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 3: LNF(XB, YF, 3); break; case 4: LNF(XB, YF, 4); break; case 6: LNF(XB, YF, 6); break; default: LNF(XB, YF, 8); }
   if (x_bf16 && y_f32) { LNF_NV(true, true) }
   else if (x_bf16) { LNF_NV(true, false) }
   else if (y_f32) { LNF_NV(false, true) }
@@ -854,18 +1073,34 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
   }
   hipStream_t st = (hipStream_t)stream;
   float* part = nsum ? ws : nullptr;
-  const int nv = ln_nv(D);
-#define LNB(AC, NVV) hipLaunchKernelGGL((k_ln_bwd<AC, NVV>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum)
-#define LNB_NV(AC) switch (nv) { case 1: LNB(AC, 1); break; case 2: LNB(AC, 2); break; case 4: LNB(AC, 4); break; case 6: LNB(AC, 6); break; default: LNB(AC, 8); }
-  if (dres_in) { LNB_NV(true) }
-  else { LNB_NV(false) }
+  const char* e = getenv("VJ_LN_V1");
+  const bool v2 = !(e && e[0] == '1') && D % 8 == 0 && lddy % 8 == 0 && ldx % 4 == 0 && ldr % 4 == 0 &&
+                  (!dres_in || ldri % 4 == 0) && (!dres_bf16 || ldrb % 8 == 0) && D <= 2048;
+  int nbl = nb;  // blocks launched (<= nb: the workspace sizing of vj_layernorm_bwd_blocks)
+  if (v2) {  // 16-B accesses (8 columns per lane-vector); a grid every CU holds at once (3 blocks)
+    const int nv8 = (D + 511) / 512;
+    nbl = nb < 768 ? nb : 768;
+    const int nb = nbl;
+#define LNB(AC, NVV) do { if (nsum == 4) hipLaunchKernelGGL((k_ln_bwd2<AC, NVV, true>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum); else hipLaunchKernelGGL((k_ln_bwd2<AC, NVV, false>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum); } while (0)
+#define LNB_NV(AC) switch (nv8) { case 1: LNB(AC, 1); break; case 2: LNB(AC, 2); break; case 3: LNB(AC, 3); break; default: LNB(AC, 4); }
+    if (dres_in) { LNB_NV(true) }
+    else { LNB_NV(false) }
 #undef LNB_NV
 #undef LNB
+  } else {
+    const int nv = ln_nv(D);
+#define LNB(AC, NVV) hipLaunchKernelGGL((k_ln_bwd<AC, NVV>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum)
+#define LNB_NV(AC) switch (nv) { case 1: LNB(AC, 1); break; case 2: LNB(AC, 2); break; case 4: LNB(AC, 4); break; case 6: LNB(AC, 6); break; default: LNB(AC, 8); }
+    if (dres_in) { LNB_NV(true) }
+    else { LNB_NV(false) }
+#undef LNB_NV
+#undef LNB
+  }
   VJ_LAUNCH_CHECK("vj_layernorm_bwd");
   // partials laid out [nb][nsum][D]: column k sums over rows of stride nsum*D
   if (nsum) {  // every requested vector in one launch (same fixed-order sums as one launch each)
     ColsumOuts o{{dgamma, dbeta, nsum > 2 ? sum_in : nullptr, nsum > 2 ? sum_out : nullptr}};
-    hipLaunchKernelGGL(k_colsum2_multi, dim3((D + 31) / 32, nsum), dim3(1024), 0, st, nb, D, ws, (long)nsum * D, o);
+    hipLaunchKernelGGL(k_colsum2_multi, dim3((D + 31) / 32, nsum), dim3(1024), 0, st, nbl, D, ws, (long)nsum * D, o);
   }
   VJ_LAUNCH_CHECK("vj_layernorm_bwd(reduce)");
   return VJ_OK;

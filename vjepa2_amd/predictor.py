@@ -114,15 +114,20 @@ class VisionTransformerPredictor(nn.Module):
             nn.init.constant_(m.weight, 1.0)
 
     # ---------------------------------------------------------------------------------------------
-    def layout(self, masks_x, masks_y, device):
+    def layout(self, masks_x, masks_y, device, n_target=None):
+        """n_target: tokens per clip of the target rows the JEPA loss gathers (loss_rows = b * n + id);
+        the clip's own token count, which is below num_patches for clips shorter than num_frames
+        (a frames-per-clip group with fewer frames than the model's maximum)."""
         mx = [m.to(device=device, dtype=torch.int64).contiguous() for m in masks_x]
         my = [m.to(device=device, dtype=torch.int64).contiguous() for m in masks_y]
-        return PredictorLayout(mx, my, self.num_patches, device)
+        return PredictorLayout(mx, my, self.num_patches if n_target is None else int(n_target), device)
 
-    def forward_ragged(self, z, masks_x, masks_y, mask_index=1, out_dtype=torch.bfloat16, layout=None):
+    def forward_ragged(self, z, masks_x, masks_y, mask_index=1, out_dtype=torch.bfloat16, layout=None,
+                       n_target=None):
         """z: encoder tokens of all mask pairs, flat [sum_m B*K_m, D] (mask order). Returns
-        (predictions of the target tokens, flat [sum_m B*Kp_m, D], PredictorLayout)."""
-        pl = layout if layout is not None else self.layout(masks_x, masks_y, z.device)
+        (predictions of the target tokens, flat [sum_m B*Kp_m, D], PredictorLayout); n_target: the
+        clips' tokens per sample (loss-row indexing, see layout())."""
+        pl = layout if layout is not None else self.layout(masks_x, masks_y, z.device, n_target=n_target)
         e = fn.run_linear(z, self.predictor_embed, out_dtype=torch.float32)
         if self.mask_tokens is None:
             raise NotImplementedError("use_mask_tokens=False predictor is not on the V-JEPA 2 path")

@@ -165,7 +165,11 @@ class JEPATrainer:
             with torch.no_grad():
                 h = self.tgt.forward_features(clips, fp8=self.fp8_target, bf16_residual=self.target_bf16_residual)
         z, _ = self.enc.forward_ragged(clips, masks_enc, out_dtype=torch.bfloat16)
-        zp, pl = self.pred.forward_ragged(z, masks_enc, masks_pred, mask_index=mask_index, out_dtype=torch.bfloat16)
+        _, Tp, Hp, Wp, _, _ = self.enc._geometry(clips)  # this group's tokens per clip (h's rows per sample)
+        if h.shape[0] != B * Tp * Hp * Wp:
+            raise RuntimeError(f"target rows {h.shape[0]} != {B} clips x {Tp * Hp * Wp} tokens")
+        zp, pl = self.pred.forward_ragged(z, masks_enc, masks_pred, mask_index=mask_index, out_dtype=torch.bfloat16,
+                                          n_target=Tp * Hp * Wp)
         if side is not None:
             main.wait_stream(side)
             h.record_stream(main)

@@ -74,6 +74,16 @@ int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k
                 long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
                 const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
                 const float* cos_t, const float* sin_t, void* stream);
+/* Backward with a dS^T workspace: the dK/dV sweep stores dS^T = (P * (dP - delta))^T of every (sequence,
+ * head) as bf16 [key][query] rows (row stride = the length rounded up to 8) and the dQ sweep is the
+ * product scale * dS K over it, instead of recomputing S, P and dP (the exponentials are evaluated once
+ * per score, not twice). Same outputs as vj_attn_bwd_fc up to the dQ sum order. fblk > 0, a NULL
+ * workspace or one smaller than vj_attn_bwd_ds_bytes take the recomputing dQ sweep. */
+int vj_attn_bwd_ds_bytes(int H, int ngroups, const int* nseq, const int* len, long* bytes);
+int vj_attn_bwd_ws(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, const void* o,
+                   long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
+                   const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
+                   const float* cos_t, const float* sin_t, int fblk, void* ds_ws, long ds_bytes, void* stream);
 /* Frame-causal (block-causal) variants for the action-conditioned predictor: with fblk > 0, token i
  * of a sequence attends to key j iff j / fblk <= i / fblk, i.e. F.scaled_dot_product_attention with the
  * attn_mask of build_action_block_causal_attention_mask (src/models/utils/modules.py:12-23; fblk = action

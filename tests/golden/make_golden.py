@@ -214,6 +214,18 @@ def gen_masks():
 
 def gen_train_steps():
     """Run the reference app/vjepa/train.py:main for 3 iterations on a micro model (CPU, fp32)."""
+    _train_steps(bf16=False)
+
+
+def gen_train_steps_bf16():
+    """The same 3 iterations of the reference's main() run inside torch.autocast("cpu", bfloat16): the
+    reference's own bf16 training precision (Linear / SDPA operands bf16, LayerNorm f32). Only the
+    losses and final weights are stored (train_steps_bf16.pt); the GPU test reads its update envelope
+    against the fp32 run (train_steps.pt)."""
+    _train_steps(bf16=True)
+
+
+def _train_steps(bf16):
     import torch.distributed as dist
     import app.vjepa.train as rtrain
 
@@ -280,11 +292,21 @@ def gen_train_steps():
         optimization=dict(ema=[0.99925, 0.99925], epochs=1, final_lr=0.000525, final_weight_decay=0.04, ipe=3,
                           ipe_scale=1.25, lr=0.000525, start_lr=0.0001, warmup=1, weight_decay=0.04),
     )
-    rtrain.main(args)
+    if bf16:
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            rtrain.main(args)
+    else:
+        rtrain.main(args)
     ck = torch.load(os.path.join(folder, "latest.pt"), map_location="cpu", weights_only=False)  # own file
 
     def strip(sd):
         return {k.replace("module.backbone.", ""): v.clone() for k, v in sd.items()}
+
+    if bf16:
+        save("train_steps_bf16.pt", dict(losses=captured["losses"], final_encoder=strip(ck["encoder"]),
+                                         final_predictor=strip(ck["predictor"]),
+                                         final_target=strip(ck["target_encoder"])))
+        return
 
     samples = []
     for s in captured["samples"][:3]:
@@ -527,3 +549,4 @@ if __name__ == "__main__":
     gen_multiclip()
     gen_ac_predictor()
     gen_vitl_autocast()
+    gen_train_steps_bf16()

@@ -208,7 +208,10 @@ def _attn_ref(q, k, v, groups, scale):
                                          # ViT-g 64x256^2: predictor n = 6013 (hd 32), context K = 2398
                                          # and the full 8192-token target sequence (hd 64)
                                          (32, 2, [(1, 6013)]), (64, 2, [(1, 2398), (1, 8192)])])
-def test_attention_fwd_bwd(hd, H, groups):
+def test_attention_fwd_bwd(hd, H, groups, monkeypatch):
+    """Forward / backward vs fp32 autograd. The backward's dQ sweep recomputes S, P, dP (default) or,
+    opt-in (VJ_ATTN_DS=1), multiplies the dS^T the dK/dV sweep stored: dK / dV bitwise equal either
+    way, dQ equal up to its sum order."""
     from vjepa2_amd import ops
 
     T = sum(n * l for n, l in groups)
@@ -231,6 +234,11 @@ def test_attention_fwd_bwd(hd, H, groups):
     # determinism
     dqkv2 = ops.attn_bwd(qkv, o, do, stats, H, hd, groups, scale)
     assert torch.equal(dqkv, dqkv2)
+    monkeypatch.setenv("VJ_ATTN_DS", "1")  # the stored-dS^T dQ sweep
+    dqkv3 = ops.attn_bwd(qkv, o, do, stats, H, hd, groups, scale)
+    monkeypatch.delenv("VJ_ATTN_DS")
+    assert torch.equal(dqkv[:, D:], dqkv3[:, D:]), "dK / dV depend on the dQ sweep"
+    _close(dqkv3[:, :D], dqkv[:, :D].float(), 1e-2, 2e-2, f"dq (stored dS^T) vs dq (recomputed) hd={hd}")
 
 
 @pytest.mark.parametrize("M,N,K,epi", [(300, 520, 1024, 1), (1100, 384, 200, 2), (64, 4096, 1024, 3), (5, 8, 3, 1)])

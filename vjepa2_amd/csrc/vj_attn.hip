@@ -20,6 +20,7 @@
 // LDS images (one per tile, read both by rows and transposed): 16-B chunk index XOR-swizzled,
 //   HD=64 (128-B rows): sw(r) = (((r>>1)&1)<<2) | ((r>>2)&3);  HD=32 (64-B rows): sw(r) = (r>>2)&3.
 // Both keep ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads bank-conflict free.
+#include <stdlib.h>
 #include <type_traits>
 
 #include "vj_common.h"
@@ -52,6 +53,7 @@ struct SeqGroups {
   int len[MAXG];
   int tok0[MAXG];
   int tiles_prefix[MAXG + 1];  // cumulative tile counts (tile size set by the kernel)
+  long ds_off[MAXG];           // backward dS^T workspace: element offset of group g's [seq][head] blocks
 };
 
 struct AttnArgs {
@@ -77,7 +79,14 @@ struct AttnArgs {
   // (build_action_block_causal_attention_mask, modules.py:12-23, with fblk = cond tokens + H*W);
   // 0 = non-causal (every key of the sequence)
   int fblk;
+  // backward: dS^T workspace (bf16). Non-null: the dK/dV sweep stores dS^T = (P * (dP - delta))^T of
+  // every (sequence, head) as [key][query] rows (stride ds_ld(len)), and the dQ sweep is a plain
+  // dQ = scale * dS K product over it (k_attn_bwd_dq_ds: no recomputation of S, P and dP)
+  bf16_t* ds;
 };
+
+// row stride (elements) of a sequence's dS^T block: the length rounded up to 8 (16-B rows)
+__device__ __host__ __forceinline__ int ds_ld(int len) { return (len + 7) & ~7; }
 
 // key limit of query qloc (keys [0, klim) are visible) and its block-uniform bounds
 __device__ __forceinline__ int fc_klim(int fblk, int qloc, int len) {
@@ -158,7 +167,7 @@ __device__ __forceinline__ void xcd_tile(int& tile, int& head) {
 
 // Locate (sequence start, length, tile index in sequence) of a flat tile id.
 __device__ __forceinline__ void locate(const SeqGroups& sg, int tile, int tiles_per_seq_div, int& seq_start,
-                                       int& len, int& t_in_seq) {
+                                       int& len, int& t_in_seq, int* grp = nullptr, int* seq = nullptr) {
   int g = 0;
 #pragma unroll
   for (int i = 1; i < MAXG; ++i)
@@ -169,6 +178,13 @@ __device__ __forceinline__ void locate(const SeqGroups& sg, int tile, int tiles_
   const int s = local / tps;
   t_in_seq = local - s * tps;
   seq_start = sg.tok0[g] + s * len;
+  if (grp) *grp = g;
+  if (seq) *seq = s;
+}
+
+// the dS^T block of (group g, sequence s, head h): [len][ds_ld(len)] bf16
+__device__ __forceinline__ long ds_block(const AttnArgs& a, int g, int s, int h, int len) {
+  return a.sg.ds_off[g] + ((long)s * a.H + h) * len * (long)ds_ld(len);
 }
 
 template <int HDP>
@@ -450,8 +466,8 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tile_id, h;
   xcd_tile(tile_id, h);
-  int seq0, len, kt;
-  locate(a.sg, tile_id, 128 * KW, seq0, len, kt);
+  int seq0, len, kt, grp, sq;
+  locate(a.sg, tile_id, 128 * KW, seq0, len, kt, &grp, &sq);
   int kloc[KW];
   bool kok[KW];
 #pragma unroll
@@ -574,6 +590,19 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn
         sacc[kw][r] = p;
         dp[kw][r] *= p;
       }
+    if (a.ds) {  // dS^T rows (this lane's key) for the dQ sweep: 4 consecutive queries per 8-B store
+      const int lp = ds_ld(len);
+#pragma unroll
+      for (int kw = 0; kw < KW; ++kw) {
+        if (!kok[kw]) continue;
+        bf16_t* row = a.ds + ds_block(a, grp, sq, h, len) + (long)kloc[kw] * lp + qt * QT + 4 * hl;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          if (qt * QT + 8 * g4 + 4 * hl < lp)
+            *(uint2*)(row + 8 * g4) = make_uint2(pack_bf2(dp[kw][4 * g4], dp[kw][4 * g4 + 1]),
+                                                 pack_bf2(dp[kw][4 * g4 + 2], dp[kw][4 * g4 + 3]));
+      }
+    }
     // dV^T += dO^T P ; dK^T += Q^T dS   (k-permuted accumulators as B operands)
     lds_wait();
 #pragma unroll
@@ -786,6 +815,105 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_b
   }
 }
 
+// dQ from the stored dS^T (a.ds, written by k_attn_bwd_dkdv): dQ^T = scale * K^T dS^T per (sequence,
+// head), block = 4 waves x 32 queries, key tiles of 64 (K rows and the dS^T tile [64 keys][128
+// queries] staged in LDS by DMA, double-buffered). Both operands come from transposed LDS reads
+// with the same key permutation (tr_frag), so no S, P or dP is recomputed: the sweep is a plain
+// MFMA product, bound by streaming dS^T once. Frame-causal layouts keep k_attn_bwd_dq (the dK/dV
+// sweep does not visit the masked query tiles, so their dS^T entries are never written).
+template <int HD>
+__global__ __launch_bounds__(256, 2) void k_attn_bwd_dq_ds(AttnArgs a) {
+  constexpr int HDP = Hd<HD>::P;
+  constexpr int KT = 64;
+  constexpr int QB = 128;                    // queries per block
+  constexpr int TBK = KT * HDP * 2;          // K tile bytes
+  constexpr int TBD = KT * QB * 2;           // dS^T tile bytes (64 rows of 256 B)
+  constexpr int STAGE = TBK + TBD;
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  LDS_AS char* smem = (LDS_AS char*)smem_raw;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int tile_id, h;
+  xcd_tile(tile_id, h);
+  int seq0, len, qt, grp, sq;
+  locate(a.sg, tile_id, QB, seq0, len, qt, &grp, &sq);
+  const int lp = ds_ld(len);
+  const int q0 = qt * QB;
+  const int qloc = q0 + wave * 32 + (lane & 31);
+  const uint32_t kbytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
+  const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.qkv + (long)seq0 * a.ld + a.k_off + h * HD, kbytes);
+  const __amdgpu_buffer_rsrc_t rd =
+      make_rsrc(a.ds + ds_block(a, grp, sq, h, len), (uint32_t)min((long)len * lp * 2, 0x7fffffffL));
+  // dS^T tile of keys [k0, k0 + 64), queries [q0, q0 + 128): 16 pieces of 1 KB (4 rows of 256 B),
+  // 4 per wave; chunk XOR-swizzled like every transposed-read image (lds_off<128>); rows past the
+  // sequence and query columns past the row end are zero-filled by the range check / VJ_OOB
+  auto stage_ds = [&](int k0, LDS_AS char* lds) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pc = wave + 4 * i;
+      const int off = pc * 1024 + lane * 16;
+      const int r = off >> 8;
+      const int c = ((off & 255) >> 4) ^ swz<128>(r);
+      const bool ok = k0 + r < len && q0 + c * 8 < lp;
+      const uint32_t voff = ok ? (uint32_t)(((long)(k0 + r) * lp + q0 + c * 8) * 2) : VJ_OOB;
+      dma16(rd, lds + pc * 1024, voff);
+    }
+  };
+  f32x16 dqt[HDP / 32];
+#pragma unroll
+  for (int d = 0; d < HDP / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dqt[d][r] = 0.f;
+  const int nkt = (len + KT - 1) / KT;
+  stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
+  stage_ds(0, smem + TBK);
+  __syncthreads();
+  auto tile_iter = [&](const int kt, auto cur_c) {
+    constexpr int cur = decltype(cur_c)::value;
+    const LDS_AS char* Ks = smem + cur * STAGE;
+    const LDS_AS char* Ds = Ks + TBK;
+    if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
+      LDS_AS char* nx = smem + (cur ^ 1) * STAGE;
+      stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
+      stage_ds((kt + 1) * KT, nx + TBK);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {  // 16-key steps
+      bf16x8 ktf[HDP / 32];
+#pragma unroll
+      for (int d = 0; d < HDP / 32; ++d) ktf[d] = tr_frag<HDP>(Ks, kk * 16, d * 32, lane);
+      const bf16x8 sf = tr_frag<128>(Ds, kk * 16, wave * 32, lane);
+      lds_wait();
+      tie(ktf);
+      bf16x8 sfa[1] = {sf};
+      tie(sfa);
+#pragma unroll
+      for (int d = 0; d < HDP / 32; ++d)
+        dqt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktf[d], sfa[0], dqt[d], 0, 0, 0);
+    }
+    __syncthreads();
+  };
+  for (int kt0 = 0; kt0 < nkt; kt0 += 2) {
+    tile_iter(kt0, std::integral_constant<int, 0>{});
+    if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
+  }
+  if (qloc >= len) return;
+  bf16_t* dq = a.dqkv + (long)(seq0 + qloc) * a.ldd + a.q_off + h * HD;
+  const bool rope = a.cos_t != nullptr;
+  const TokPos tp = rope ? tok_pos(a, seq0 + qloc) : TokPos{0, 0, 0};
+#pragma unroll
+  for (int d = 0; d < HDP / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dqt[d][r] *= a.scale;
+  if (rope) rope_inv_rows<HD>(a, tp, lane, dqt);
+#pragma unroll
+  for (int d = 0; d < HDP / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const int col = d * 32 + acc_row(r, lane);
+      if (col < HD) *(uint32_t*)(dq + col) = pack_bf2(dqt[d][r], dqt[d][r + 1]);
+    }
+}
+
 int fill_groups(SeqGroups& sg, int ngroups, const int* nseq, const int* len, int tile, long T) {
   VJ_CHECK_ARG(ngroups >= 1 && ngroups <= MAXG, "attention: 1..%d sequence groups supported (got %d)", MAXG, ngroups);
   sg.ngroups = ngroups;
@@ -853,11 +981,54 @@ extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q
                         stream);
 }
 
+// dS^T workspace of the backward: sum over groups of nseq * H * len * ds_ld(len) bf16
+static long ds_elems(int H, int ngroups, const int* nseq, const int* len, long* off) {
+  long tot = 0;
+  for (int g = 0; g < MAXG; ++g) {
+    if (off) off[g] = tot;
+    if (g < ngroups) tot += (long)nseq[g] * H * len[g] * (((long)len[g] + 7) & ~7L);
+  }
+  return tot;
+}
+
+extern "C" int vj_attn_bwd_ds_bytes(int H, int ngroups, const int* nseq, const int* len, long* bytes) {
+  VJ_CHECK_ARG(bytes && nseq && len && ngroups >= 1 && ngroups <= MAXG, "vj_attn_bwd_ds_bytes: bad arguments");
+  *bytes = 2 * ds_elems(H, ngroups, nseq, len, nullptr);
+  return VJ_OK;
+}
+
+static int attn_bwd_impl(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                         const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
+                         float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
+                         int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t, int fblk,
+                         void* ds_ws, long ds_bytes, void* stream);
+
 extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
                               const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
                               long ldd, float scale, int ngroups, const int* nseq, const int* len,
                               const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t,
                               const float* sin_t, int fblk, void* stream) {
+  return attn_bwd_impl(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
+                       nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, fblk, nullptr, 0, stream);
+}
+
+// As vj_attn_bwd_fc with a dS^T workspace (vj_attn_bwd_ds_bytes): the dK/dV sweep stores dS^T and the
+// dQ sweep multiplies it by K instead of recomputing S, P and dP (non-causal layouts; fblk > 0 or a
+// NULL / short workspace take the recomputing dQ sweep).
+extern "C" int vj_attn_bwd_ws(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                              const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
+                              long ldd, float scale, int ngroups, const int* nseq, const int* len,
+                              const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t,
+                              const float* sin_t, int fblk, void* ds_ws, long ds_bytes, void* stream) {
+  return attn_bwd_impl(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
+                       nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, fblk, ds_ws, ds_bytes, stream);
+}
+
+static int attn_bwd_impl(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                         const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
+                         float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
+                         int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t, int fblk,
+                         void* ds_ws, long ds_bytes, void* stream) {
   if (T == 0) return VJ_OK;
   int rc = check_common(H, hd, ld, ldo);
   if (rc) return rc;
@@ -888,6 +1059,44 @@ extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, in
   const long nth = (long)T * H;
   const int dblocks = (int)((nth + 255) / 256);
   const dim3 gk(ak.sg.tiles_prefix[MAXG], H), gq(aq.sg.tiles_prefix[MAXG], H);
+  const char* env = getenv("VJ_ATTN_DS");
+  // opt-in (VJ_ATTN_DS=1): measured slower than recomputing dS in the dQ sweep (attention)
+  const bool use_ds = ds_ws && fblk == 0 && env && env[0] == '1' &&
+                      ds_bytes >= 2 * ds_elems(H, ngroups, nseq, len, nullptr) && ((uintptr_t)ds_ws & 15) == 0;
+  if (use_ds) {  // dK/dV sweep storing dS^T, then dQ = scale * dS K over it
+    ak.ds = (bf16_t*)ds_ws;
+    ds_elems(H, ngroups, nseq, len, ak.sg.ds_off);
+    AttnArgs ad = a;
+    ad.ds = ak.ds;
+    rc = fill_groups(ad.sg, ngroups, nseq, len, 128, T);
+    if (rc) return rc;
+    ds_elems(H, ngroups, nseq, len, ad.sg.ds_off);
+    const dim3 gd(ad.sg.tiles_prefix[MAXG], H);
+    switch (hd) {
+      case 64:
+        hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64>), gk, dim3(256), 0, st, ak);
+        hipLaunchKernelGGL(k_attn_bwd_dq_ds<64>, gd, dim3(256), 0, st, ad);
+        break;
+      case 32:
+        hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32>), gk, dim3(256), 0, st, ak);
+        hipLaunchKernelGGL(k_attn_bwd_dq_ds<32>, gd, dim3(256), 0, st, ad);
+        break;
+      case 80:
+        hipLaunchKernelGGL(k_attn_delta<80>, dim3(dblocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<80, 1>), gk, dim3(256), 0, st, ak);
+        hipLaunchKernelGGL(k_attn_bwd_dq_ds<80>, gd, dim3(256), 0, st, ad);
+        break;
+      default:
+        hipLaunchKernelGGL(k_attn_delta<88>, dim3(dblocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<88, 1>), gk, dim3(256), 0, st, ak);
+        hipLaunchKernelGGL(k_attn_bwd_dq_ds<88>, gd, dim3(256), 0, st, ad);
+        break;
+    }
+    VJ_LAUNCH_CHECK("vj_attn_bwd");
+    return VJ_OK;
+  }
   switch (hd) {
     case 64:
       hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);

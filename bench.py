@@ -290,13 +290,14 @@ def _pmc_traffic(label, workload):
     measurement is for another kernel or another workload."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
     try:
-        tr = json.load(open(path))
+        data = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if tr.get("kernel") != label or tr.get("workload", "vit_large 16x256^2 B=24") != workload:
-        return None
-    tr["source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py)"
-    return tr
+    for tr in data if isinstance(data, list) else [data]:  # one entry per (kernel, workload)
+        if tr.get("kernel") == label and tr.get("workload", "vit_large 16x256^2 B=24") == workload:
+            tr["source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py)"
+            return tr
+    return None
 
 
 def _cpu_model():

@@ -67,23 +67,25 @@ int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmaj
 int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o, long ldo,
                 float* stats, float scale, int ngroups, const int* nseq, const int* len, void* stream);
 /* Backward: writes dq/dk/dv (bf16) into dqkv at the same column offsets; uses stats[0] and writes
- * stats[1] = rowsum(dO * O). Deterministic (separate dK/dV and dQ sweeps, no atomics). With cos_t
+ * stats[1] = -rowsum(dO * O). Deterministic (separate dK/dV and dQ sweeps, no atomics). With cos_t
  * non-NULL the transpose of the 3-axis RoPE (see vj_rope) is applied to dq and dk before the store,
  * i.e. dqkv is the gradient w.r.t. the UN-rotated q, k (the QKV projection output). */
 int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, const void* o,
                 long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
                 const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
                 const float* cos_t, const float* sin_t, void* stream);
-/* Backward with a dS^T workspace: the dK/dV sweep stores dS^T = (P * (dP - delta))^T of every (sequence,
- * head) as bf16 [key][query] rows (row stride = the length rounded up to 8) and the dQ sweep is the
- * product scale * dS K over it, instead of recomputing S, P and dP (the exponentials are evaluated once
- * per score, not twice). Same outputs as vj_attn_bwd_fc up to the dQ sum order. fblk > 0, a NULL
- * workspace or one smaller than vj_attn_bwd_ds_bytes take the recomputing dQ sweep. */
-int vj_attn_bwd_ds_bytes(int H, int ngroups, const int* nseq, const int* len, long* bytes);
+/* Backward with a workspace (bytes from vj_attn_bwd_ws_bytes): with VJ_ATTN_FUSED=1 in the
+ * environment (opt-in: measured slower than the two sweeps), head dims 32 and 64 without a
+ * frame-causal mask run the fused backward: the dK/dV sweep also multiplies each query tile's dS by
+ * the block's K rows (dQ partial per 128-/256-key block, f32 in the workspace) and a reduce pass sums
+ * the blocks in a fixed order, so S, P and dP are evaluated once per score instead of twice. Same
+ * outputs as vj_attn_bwd_fc up to the dQ sum order; still deterministic. fblk > 0, head dims 80 / 88
+ * and a NULL or short workspace take the two sweeps. */
+int vj_attn_bwd_ws_bytes(int H, int hd, int ngroups, const int* nseq, const int* len, long* bytes);
 int vj_attn_bwd_ws(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, const void* o,
                    long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
                    const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
-                   const float* cos_t, const float* sin_t, int fblk, void* ds_ws, long ds_bytes, void* stream);
+                   const float* cos_t, const float* sin_t, int fblk, void* ws, long ws_bytes, void* stream);
 /* Frame-causal (block-causal) variants for the action-conditioned predictor: with fblk > 0, token i
  * of a sequence attends to key j iff j / fblk <= i / fblk, i.e. F.scaled_dot_product_attention with the
  * attn_mask of build_action_block_causal_attention_mask (src/models/utils/modules.py:12-23; fblk = action

@@ -1,6 +1,6 @@
 """HBM traffic per launch of the bench's dominant kernel, from two rocprofv3 PMC passes over bench.py.
 
-    python tools/traffic.py <fetch_pass_dir> <write_pass_dir> <label> <out.json>
+    python tools/traffic.py <fetch_pass_dir> <write_pass_dir> <label> <out.json> [workload]
 
 `label` is bench.py's kernel label (e.g. "k_gemm<1,1,EPI_F32_RESID>"); it is matched against the
 rocprofv3 kernel names (k_gemm256<true, true, 2, BN> for every tile width BN).
@@ -52,7 +52,14 @@ def main():
            "hbm_bytes_per_launch": round((2.0 * fkib + wkib) * 1024.0),
            "correction": "bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (KiB units; gfx950 FETCH_SIZE "
                          "counts half of 16B/lane streaming reads)"}
-    json.dump(res, open(out, "w"), indent=1)
+    # profiles/traffic.json holds one entry per (kernel, workload): replace this one's, keep the others
+    try:
+        old = json.load(open(out))
+        old = old if isinstance(old, list) else [old]
+    except (OSError, ValueError):
+        old = []
+    keep = [e for e in old if (e.get("kernel"), e.get("workload")) != (label, workload)]
+    json.dump(keep + [res], open(out, "w"), indent=1)
     print(json.dumps(res))
 
 

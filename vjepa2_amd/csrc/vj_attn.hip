@@ -53,7 +53,7 @@ struct SeqGroups {
   int len[MAXG];
   int tok0[MAXG];
   int tiles_prefix[MAXG + 1];  // cumulative tile counts (tile size set by the kernel)
-  long ds_off[MAXG];           // backward dS^T workspace: element offset of group g's [seq][head] blocks
+  long part_off[MAXG];         // fused backward: float offset of group g's dQ partials [seq][head][kblock]
 };
 
 struct AttnArgs {
@@ -79,14 +79,13 @@ struct AttnArgs {
   // (build_action_block_causal_attention_mask, modules.py:12-23, with fblk = cond tokens + H*W);
   // 0 = non-causal (every key of the sequence)
   int fblk;
-  // backward: dS^T workspace (bf16). Non-null: the dK/dV sweep stores dS^T = (P * (dP - delta))^T of
-  // every (sequence, head) as [key][query] rows (stride ds_ld(len)), and the dQ sweep is a plain
-  // dQ = scale * dS K product over it (k_attn_bwd_dq_ds: no recomputation of S, P and dP)
-  bf16_t* ds;
+  // fused backward (k_attn_bwd_dkdv<HD, KW, true>): per key block, dQ partial = dS K over the block's
+  // keys, f32 [query][hd] per (sequence, head, key block) at part_off; k_attn_dq_reduce sums them
+  float* dqp;
+  // dQ sweep: computes delta = rowsum(dO * O) itself (from its dO fragments and O) and writes -delta to
+  // stats for the dK/dV sweep that runs after it (no separate k_attn_delta launch)
+  int dq_delta;
 };
-
-// row stride (elements) of a sequence's dS^T block: the length rounded up to 8 (16-B rows)
-__device__ __host__ __forceinline__ int ds_ld(int len) { return (len + 7) & ~7; }
 
 // key limit of query qloc (keys [0, klim) are visible) and its block-uniform bounds
 __device__ __forceinline__ int fc_klim(int fblk, int qloc, int len) {
@@ -182,11 +181,6 @@ __device__ __forceinline__ void locate(const SeqGroups& sg, int tile, int tiles_
   if (seq) *seq = s;
 }
 
-// the dS^T block of (group g, sequence s, head h): [len][ds_ld(len)] bf16
-__device__ __forceinline__ long ds_block(const AttnArgs& a, int g, int s, int h, int len) {
-  return a.sg.ds_off[g] + ((long)s * a.H + h) * len * (long)ds_ld(len);
-}
-
 template <int HDP>
 __device__ __forceinline__ int swz(int r) {
   if constexpr (HDP == 64) return (((r >> 1) & 1) << 2) | ((r >> 2) & 3);
@@ -246,6 +240,52 @@ __device__ __forceinline__ bf16x8 tr_frag(const LDS_AS char* lds, int kb, int cb
   const s16x4 hi = ds_read_tr16_async(lds + lds_off<HDP>(r1, col >> 3) + within);
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// ---- 16x16x32 operand images of the fused dQ product (k_attn_bwd_dkdv<HD, KW, true>): key-major
+// rows of RB bytes (64: 32 bf16, 128: 64 bf16), 32-B column pairs XOR-swizzled by row so that a
+// transposed fragment read (per half-wave: 8 rows x 32 B at one column pair) hits every bank once.
+template <int RB>
+__device__ __forceinline__ int pair_swz(int r) {
+  return RB == 64 ? ((r >> 3) & 1) : (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+}
+template <int RB>
+__device__ __forceinline__ int img_off(int r, int col) {  // byte offset of bf16 element col of row r
+  return r * RB + (((col >> 4) ^ pair_swz<RB>(r)) << 5) + ((col & 15) << 1);
+}
+// 16x16x32 MFMA operand from a key-major image X[k][m]: lane l holds X[kb + 8(l>>4) + j][mb + (l&15)],
+// j = 0..7 — the same key order for the A (K^T) and B (dS^T) operands, so the product sums the same
+// keys. The swizzle depends only on row bits 1 and 3, so for kb a multiple of 32 the address is the
+// lane part img_lane(mb) (computed once per use site) plus kb * RB. Asm reads: lds_wait() + tie().
+template <int RB>
+__device__ __forceinline__ int img_lane(int mb, int lane) {
+  const int gi = lane & 15;
+  return img_off<RB>(8 * (lane >> 4) + (gi >> 2), mb + 4 * (gi & 3));
+}
+template <int RB>
+__device__ __forceinline__ bf16x8 img_frag(const LDS_AS char* img, int loff, int kb) {
+  const s16x4 lo = ds_read_tr16_async(img + loff + kb * RB);
+  const s16x4 hi = ds_read_tr16_async(img + loff + (kb + 4) * RB);
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// DMA ROWS rows of HD bf16 (from token row0; rows past nvalid zero-filled) into such an image
+template <int HD, int ROWS>
+__device__ __forceinline__ void stage_img(__amdgpu_buffer_rsrc_t rs, long ld, int row0, int nvalid,
+                                          LDS_AS char* lds, int wave, int lane) {
+  constexpr int RB = HD * 2;
+  constexpr int PIECES = ROWS * RB / 1024;
+  static_assert(PIECES % 4 == 0, "whole 1-KB pieces per wave");
+#pragma unroll
+  for (int i = 0; i < PIECES / 4; ++i) {
+    const int p = wave + 4 * i;
+    const int off = p * 1024 + lane * 16;
+    const int r = off / RB;
+    const int pc = (off - r * RB) >> 4;                              // physical 16-B chunk
+    const int c = (((pc >> 1) ^ pair_swz<RB>(r)) << 1) | (pc & 1);  // the logical chunk it holds
+    const uint32_t voff = row0 + r < nvalid ? (uint32_t)(((long)(row0 + r) * ld + c * 8) * 2) : VJ_OOB;
+    dma16(rs, lds + p * 1024, voff);
+  }
 }
 
 // Accumulator registers 8s..8s+7 -> bf16 operand fragment.
@@ -450,19 +490,34 @@ __global__ void k_attn_delta(AttnArgs a) {
 // dK/dV: block = 4 waves x (32 KW) keys; sweep query tiles of 32 (Q, dO, lse, delta staged in LDS).
 // Each wave owns KW 32-key tiles (key tile kw of wave w: keys kw*128 + w*32 + 0..31 of the block),
 // so every staged Q / dO fragment feeds KW independent MFMA chains per barrier.
+// DQ (fused dQ, head dims 32 / 64, non-causal): the block's K rows sit in an LDS image; each query
+// tile's dS (bf16, the values the dK product uses) goes to a key-major LDS image, and after the
+// tile's barrier the block computes its dQ partial dQ^T = K^T dS^T over its own keys with 16x16x32
+// MFMAs (wave w: output blocks w, w+4 of the (hd/16) x 2 grid of 16x16 blocks), stored f32 to
+// a.dqp; k_attn_dq_reduce sums the key blocks in a fixed order. No recomputation of S, P, dP.
+// fused dQ product serialised before the S / dP MFMAs instead of interleaved with them (measurement)
+#ifndef VJ_ATTN_DQ_SERIAL
+#define VJ_ATTN_DQ_SERIAL 0
+#endif
 // dK/dV workgroups per CU the register budget is sized for (head dims <= 64); 1 = no bound
 #ifndef VJ_ATTN_DKDV_OCC
 #define VJ_ATTN_DKDV_OCC 1
 #endif
-template <int HD, int KW>
-__global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn_bwd_dkdv(AttnArgs a) {
+template <int HD, int KW, bool DQ = false>
+__global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn_bwd_dkdv(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
+  static_assert(!DQ || HD == 32 || HD == 64, "fused dQ: head dims 32 and 64");
   constexpr int QT = 32;
   constexpr int TB = QT * HDP * 2;
   // per stage: Q tile, dO tile, 32 lse + 32 delta floats
   constexpr int STAGE = 2 * TB + 256;
-  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  constexpr int NK = 128 * KW;               // keys per block
+  constexpr int KIMG = DQ ? NK * HD * 2 : 0;  // K image of the block's keys (fused dQ)
+  constexpr int DSB = DQ ? NK * 64 : 0;       // one dS image: [NK keys][32 queries] bf16
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE + KIMG + 2 * DSB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
+  [[maybe_unused]] LDS_AS char* kimg = smem + 2 * STAGE;
+  [[maybe_unused]] LDS_AS char* dsimg = kimg + KIMG;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tile_id, h;
   xcd_tile(tile_id, h);
@@ -497,6 +552,43 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn
   const __amdgpu_buffer_rsrc_t rs =
       make_rsrc(a.stats + (long)h * a.T + seq0, (uint32_t)min(((long)a.H * a.T + len) * 4, 0x7fffffffL));
   const long dstat = (long)a.H * a.T;  // element distance lse -> delta
+  [[maybe_unused]] long pbase = 0;
+  if constexpr (DQ) {
+    const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.qkv + (long)seq0 * a.ld + a.k_off + h * HD, qbytes);
+    stage_img<HD, NK>(rk, a.ld, kt * NK, len, kimg, wave, lane);  // published by the first barrier
+    const int nkb = (len + NK - 1) / NK;
+    pbase = a.sg.part_off[grp] + ((long)(sq * a.H + h) * nkb + kt) * len * HD;
+  }
+  // fused dQ of query tile `qtile` from the dS image D (all 4 waves' keys: after the tile's barrier)
+  [[maybe_unused]] auto dq_tile = [&](const int qtile, const LDS_AS char* D) {
+    constexpr int NB = HD / 16 * 2;  // 16x16 blocks of dQ^T: hd / 16 row blocks x 2 query halves
+#pragma unroll
+    for (int bi = 0; bi < NB / 4; ++bi) {
+      const int b = wave + 4 * bi;
+      const int m0 = 16 * (b >> 1), n0 = 16 * (b & 1);
+      int le = lane;
+      asm volatile("" : "+v"(le));  // per-call lane addressing (not hoisted to live across the sweep)
+      const int la = img_lane<2 * HD>(m0, le), lb = img_lane<64>(n0, le);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k2 = 0; k2 < NK / 64; ++k2) {  // two 32-key steps per LDS wait
+        bf16x8 fa[2], fb[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          fa[u] = img_frag<2 * HD>(kimg, la, 64 * k2 + 32 * u);
+          fb[u] = img_frag<64>(D, lb, 64 * k2 + 32 * u);
+        }
+        lds_wait();
+        tie(fa);
+        tie(fb);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u], fb[u], acc, 0, 0, 0);
+      }
+      // lane: dQ^T rows m0 + 4(lane>>4) + 0..3 (head dims) of query n0 + (lane&15)
+      const int q = qtile * QT + n0 + (lane & 15);
+      if (q < len) *(f32x4*)(a.dqp + pbase + (long)q * HD + m0 + 4 * (lane >> 4)) = acc;
+    }
+  };
 
   f32x16 dvt[KW][HDP / 32], dkt[KW][HDP / 32];
 #pragma unroll
@@ -558,13 +650,65 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn
         dp[kw][r] = dl;
       }
     }
+    if constexpr (!DQ || VJ_ATTN_DQ_SERIAL) {
+      if constexpr (DQ) {  // the previous query tile's dS (image cur ^ 1, complete since the last barrier)
+        if (qt > qt_first) dq_tile(qt - 1, dsimg + (cur ^ 1) * DSB);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
-    for (int s = 0; s < HDP / 16; ++s)
+      for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
-      for (int kw = 0; kw < KW; ++kw) {
+        for (int kw = 0; kw < KW; ++kw) {
+          sacc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[kw][s], sacc[kw], 0, 0, 0);
+          dp[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[kw][s], dp[kw], 0, 0, 0);
+        }
+    } else {
+      // This tile's S / dP MFMAs interleaved with the previous tile's fused dQ product: dQ chunk c
+      // (two 32-key steps of one 16x16 block) is read from LDS one step ahead, into alternating
+      // fragment registers, and multiplied after the (s, kw) pair c of S / dP, so the transposed-read
+      // latency hides under those MFMAs.
+      constexpr int NSD = HDP / 16 * KW;
+      constexpr int NKC = NK / 64;                  // chunks per 16x16 block
+      constexpr int NCH = (HD / 16 * 2 / 4) * NKC;  // chunks per wave
+      static_assert(NSD == NCH, "one dQ chunk per S / dP MFMA pair");
+      const bool dqp = qt > qt_first;
+      const LDS_AS char* D = dsimg + (cur ^ 1) * DSB;
+      int le = lane;
+      asm volatile("" : "+v"(le));
+      bf16x8 fa[2][2], fb[2][2];
+      f32x4 dacc = {0.f, 0.f, 0.f, 0.f};
+      auto reads = [&](int c, bf16x8 (&xa)[2], bf16x8 (&xb)[2]) {
+        const int b = wave + 4 * (c / NKC), k2 = c % NKC;
+        const int la = img_lane<2 * HD>(16 * (b >> 1), le), lb = img_lane<64>(16 * (b & 1), le);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          xa[u] = img_frag<2 * HD>(kimg, la, 64 * k2 + 32 * u);
+          xb[u] = img_frag<64>(D, lb, 64 * k2 + 32 * u);
+        }
+      };
+      if (dqp) reads(0, fa[0], fb[0]);
+#pragma unroll
+      for (int c = 0; c < NSD; ++c) {
+        const int s = c / KW, kw = c % KW;
         sacc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[kw][s], sacc[kw], 0, 0, 0);
         dp[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[kw][s], dp[kw], 0, 0, 0);
+        if (dqp) {
+          lds_wait();
+          tie(fa[c & 1]);
+          tie(fb[c & 1]);
+          if (c + 1 < NCH) reads(c + 1, fa[(c + 1) & 1], fb[(c + 1) & 1]);
+#pragma unroll
+          for (int u = 0; u < 2; ++u)
+            dacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c & 1][u], fb[c & 1][u], dacc, 0, 0, 0);
+          if (c % NKC == NKC - 1) {  // block done: store its partial
+            const int b = wave + 4 * (c / NKC);
+            const int q = (qt - 1) * QT + 16 * (b & 1) + (le & 15);
+            if (q < len) *(f32x4*)(a.dqp + pbase + (long)q * HD + 16 * (b >> 1) + 4 * (le >> 4)) = dacc;
+            dacc = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
       }
+    }
     bf16x8 dtf[2][HDP / 32], qtf[2][HDP / 32];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -590,17 +734,22 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn
         sacc[kw][r] = p;
         dp[kw][r] *= p;
       }
-    if (a.ds) {  // dS^T rows (this lane's key) for the dQ sweep: 4 consecutive queries per 8-B store
-      const int lp = ds_ld(len);
+    if constexpr (DQ) {  // dS rows (this lane's key, 4 consecutive queries per 8-B write) into image cur;
+      // keys past the end get 0 (their K rows are zero, but their P can overflow: no inf * 0)
+      LDS_AS char* D = dsimg + cur * DSB + wave * 32 * 64;
+      int le = lane;
+      asm volatile("" : "+v"(le));
 #pragma unroll
       for (int kw = 0; kw < KW; ++kw) {
-        if (!kok[kw]) continue;
-        bf16_t* row = a.ds + ds_block(a, grp, sq, h, len) + (long)kloc[kw] * lp + qt * QT + 4 * hl;
+        const int row = kw * 128 + (le & 31);  // + wave * 32 in D (swizzle: row bits 1 and 3 only)
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4)
-          if (qt * QT + 8 * g4 + 4 * hl < lp)
-            *(uint2*)(row + 8 * g4) = make_uint2(pack_bf2(dp[kw][4 * g4], dp[kw][4 * g4 + 1]),
-                                                 pack_bf2(dp[kw][4 * g4 + 2], dp[kw][4 * g4 + 3]));
+        for (int g4 = 0; g4 < 4; ++g4) {
+          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+          const u32x2 v = kok[kw] ? u32x2{pack_bf2(dp[kw][4 * g4], dp[kw][4 * g4 + 1]),
+                                          pack_bf2(dp[kw][4 * g4 + 2], dp[kw][4 * g4 + 3])}
+                                  : u32x2{0u, 0u};
+          *(LDS_AS u32x2*)(D + img_off<64>(row, 8 * g4 + 4 * hl)) = v;
+        }
       }
     }
     // dV^T += dO^T P ; dK^T += Q^T dS   (k-permuted accumulators as B operands)
@@ -628,6 +777,7 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn
     tile_iter(qt0, std::integral_constant<int, 0>{});
     if (qt0 + 1 < nqt) tile_iter(qt0 + 1, std::integral_constant<int, 1>{});
   }
+  if constexpr (DQ) dq_tile(nqt - 1, dsimg + ((nqt - 1 - qt_first) & 1) * DSB);
 #pragma unroll
   for (int kw = 0; kw < KW; ++kw) {
     if (!kok[kw]) continue;
@@ -690,7 +840,21 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_b
       gf[qw][s] = gload8(grow + 16 * s + 8 * hl, qok[qw] && 16 * s + 8 * hl < HD);
     }
     lse2[qw] = qok[qw] ? a.stats[(long)h * a.T + seq0 + qloc[qw]] : 0.f;
-    dl[qw] = qok[qw] ? a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc[qw]] : 0.f;
+    if (a.dq_delta) {  // -delta = -sum_d dO * O: lanes q and q + 32 hold the two halves of each 16-dim step
+      const bf16_t* orow = a.o + (long)(seq0 + qloc[qw]) * a.ldo + h * HD;
+      float sd = 0.f;
+#pragma unroll
+      for (int s = 0; s < HDP / 16; ++s) {
+        const bf16x8 ov = gload8(orow + 16 * s + 8 * hl, qok[qw] && 16 * s + 8 * hl < HD);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sd = fmaf((float)gf[qw][s][j], (float)ov[j], sd);
+      }
+      sd += __shfl_xor(sd, 32, 64);
+      dl[qw] = qok[qw] ? -sd : 0.f;
+      if (qok[qw] && hl == 0) a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc[qw]] = -sd;
+    } else {
+      dl[qw] = qok[qw] ? a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc[qw]] : 0.f;
+    }
   }
 
   const uint32_t bytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
@@ -815,103 +979,48 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_b
   }
 }
 
-// dQ from the stored dS^T (a.ds, written by k_attn_bwd_dkdv): dQ^T = scale * K^T dS^T per (sequence,
-// head), block = 4 waves x 32 queries, key tiles of 64 (K rows and the dS^T tile [64 keys][128
-// queries] staged in LDS by DMA, double-buffered). Both operands come from transposed LDS reads
-// with the same key permutation (tr_frag), so no S, P or dP is recomputed: the sweep is a plain
-// MFMA product, bound by streaming dS^T once. Frame-causal layouts keep k_attn_bwd_dq (the dK/dV
-// sweep does not visit the masked query tiles, so their dS^T entries are never written).
+// Inverse RoPE of one (d, d + 1) pair of a row (the scalar form of rope_inv_rows)
 template <int HD>
-__global__ __launch_bounds__(256, 2) void k_attn_bwd_dq_ds(AttnArgs a) {
-  constexpr int HDP = Hd<HD>::P;
-  constexpr int KT = 64;
-  constexpr int QB = 128;                    // queries per block
-  constexpr int TBK = KT * HDP * 2;          // K tile bytes
-  constexpr int TBD = KT * QB * 2;           // dS^T tile bytes (64 rows of 256 B)
-  constexpr int STAGE = TBK + TBD;
-  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
-  LDS_AS char* smem = (LDS_AS char*)smem_raw;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int tile_id, h;
-  xcd_tile(tile_id, h);
-  int seq0, len, qt, grp, sq;
-  locate(a.sg, tile_id, QB, seq0, len, qt, &grp, &sq);
-  const int lp = ds_ld(len);
-  const int q0 = qt * QB;
-  const int qloc = q0 + wave * 32 + (lane & 31);
-  const uint32_t kbytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
-  const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.qkv + (long)seq0 * a.ld + a.k_off + h * HD, kbytes);
-  const __amdgpu_buffer_rsrc_t rd =
-      make_rsrc(a.ds + ds_block(a, grp, sq, h, len), (uint32_t)min((long)len * lp * 2, 0x7fffffffL));
-  // dS^T tile of keys [k0, k0 + 64), queries [q0, q0 + 128): 16 pieces of 1 KB (4 rows of 256 B),
-  // 4 per wave; chunk XOR-swizzled like every transposed-read image (lds_off<128>); rows past the
-  // sequence and query columns past the row end are zero-filled by the range check / VJ_OOB
-  auto stage_ds = [&](int k0, LDS_AS char* lds) {
+__device__ __forceinline__ void rope_inv_pair(const AttnArgs& a, const TokPos& tp, int d, float& x0, float& x1) {
+  constexpr int half = (HD / 3) / 2, sw = 2 * half;
+  if (d >= 3 * sw) return;
+  const int ax = d / sw, js = d - ax * sw;
+  const int pos = (ax == 0 ? tp.fr : (ax == 1 ? tp.hr : tp.wc)) * half;
+  const int i0 = pos + js % half, i1 = pos + (js + 1) % half;
+  const float c0 = a.cos_t[i0], s0 = a.sin_t[i0], c1 = a.cos_t[i1], s1 = a.sin_t[i1];
+  const float y0 = x0 * c0 + x1 * s1, y1 = -x0 * s0 + x1 * c1;
+  x0 = y0;
+  x1 = y1;
+}
+
+// Fused backward, second pass: dQ = scale * (sum over the key blocks of the dQ partials, in block
+// order), inverse RoPE, bf16 into the q columns of dqkv. One thread per (token, head, 4 head dims).
+template <int HD, int NK>
+__global__ void k_attn_dq_reduce(AttnArgs a) {
+  constexpr int G = HD / 4;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)a.T * a.H * G) return;
+  const int dg = (int)(i % G);
+  const long th = i / G;
+  const int h = (int)(th % a.H), t = (int)(th / a.H);
+  int g = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int pc = wave + 4 * i;
-      const int off = pc * 1024 + lane * 16;
-      const int r = off >> 8;
-      const int c = ((off & 255) >> 4) ^ swz<128>(r);
-      const bool ok = k0 + r < len && q0 + c * 8 < lp;
-      const uint32_t voff = ok ? (uint32_t)(((long)(k0 + r) * lp + q0 + c * 8) * 2) : VJ_OOB;
-      dma16(rd, lds + pc * 1024, voff);
-    }
-  };
-  f32x16 dqt[HDP / 32];
-#pragma unroll
-  for (int d = 0; d < HDP / 32; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dqt[d][r] = 0.f;
-  const int nkt = (len + KT - 1) / KT;
-  stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
-  stage_ds(0, smem + TBK);
-  __syncthreads();
-  auto tile_iter = [&](const int kt, auto cur_c) {
-    constexpr int cur = decltype(cur_c)::value;
-    const LDS_AS char* Ks = smem + cur * STAGE;
-    const LDS_AS char* Ds = Ks + TBK;
-    if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
-      LDS_AS char* nx = smem + (cur ^ 1) * STAGE;
-      stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
-      stage_ds((kt + 1) * KT, nx + TBK);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {  // 16-key steps
-      bf16x8 ktf[HDP / 32];
-#pragma unroll
-      for (int d = 0; d < HDP / 32; ++d) ktf[d] = tr_frag<HDP>(Ks, kk * 16, d * 32, lane);
-      const bf16x8 sf = tr_frag<128>(Ds, kk * 16, wave * 32, lane);
-      lds_wait();
-      tie(ktf);
-      bf16x8 sfa[1] = {sf};
-      tie(sfa);
-#pragma unroll
-      for (int d = 0; d < HDP / 32; ++d)
-        dqt[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktf[d], sfa[0], dqt[d], 0, 0, 0);
-    }
-    __syncthreads();
-  };
-  for (int kt0 = 0; kt0 < nkt; kt0 += 2) {
-    tile_iter(kt0, std::integral_constant<int, 0>{});
-    if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
+  for (int j = 1; j < MAXG; ++j)
+    if (j < a.sg.ngroups && t >= a.sg.tok0[j]) g = j;
+  const int len = a.sg.len[g], loc = t - a.sg.tok0[g];
+  const int s = loc / len, q = loc - s * len;
+  const int nkb = (len + NK - 1) / NK;
+  const float* p = a.dqp + a.sg.part_off[g] + (long)(s * a.H + h) * nkb * len * HD + (long)q * HD + 4 * dg;
+  f32x4 acc = *(const f32x4*)p;
+  for (int kb = 1; kb < nkb; ++kb) acc += *(const f32x4*)(p + (long)kb * len * HD);
+  float x[4] = {acc[0] * a.scale, acc[1] * a.scale, acc[2] * a.scale, acc[3] * a.scale};
+  if (a.cos_t) {
+    const TokPos tp = tok_pos(a, t);
+    rope_inv_pair<HD>(a, tp, 4 * dg, x[0], x[1]);
+    rope_inv_pair<HD>(a, tp, 4 * dg + 2, x[2], x[3]);
   }
-  if (qloc >= len) return;
-  bf16_t* dq = a.dqkv + (long)(seq0 + qloc) * a.ldd + a.q_off + h * HD;
-  const bool rope = a.cos_t != nullptr;
-  const TokPos tp = rope ? tok_pos(a, seq0 + qloc) : TokPos{0, 0, 0};
-#pragma unroll
-  for (int d = 0; d < HDP / 32; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dqt[d][r] *= a.scale;
-  if (rope) rope_inv_rows<HD>(a, tp, lane, dqt);
-#pragma unroll
-  for (int d = 0; d < HDP / 32; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const int col = d * 32 + acc_row(r, lane);
-      if (col < HD) *(uint32_t*)(dq + col) = pack_bf2(dqt[d][r], dqt[d][r + 1]);
-    }
+  *(uint2*)(a.dqkv + (long)t * a.ldd + a.q_off + h * HD + 4 * dg) =
+      make_uint2(pack_bf2(x[0], x[1]), pack_bf2(x[2], x[3]));
 }
 
 int fill_groups(SeqGroups& sg, int ngroups, const int* nseq, const int* len, int tile, long T) {
@@ -981,19 +1090,23 @@ extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q
                         stream);
 }
 
-// dS^T workspace of the backward: sum over groups of nseq * H * len * ds_ld(len) bf16
-static long ds_elems(int H, int ngroups, const int* nseq, const int* len, long* off) {
+// keys per block of the fused backward (0: no fused kernel for this head dim)
+static int fused_nk(int hd) { return hd == 32 ? 128 * VJ_ATTN_KW32 : hd == 64 ? 128 * VJ_ATTN_KW64 : 0; }
+
+// fused-backward dQ partials: sum over groups of nseq * H * ceil(len / NK) * len * hd floats
+static long part_elems(int H, int hd, int ngroups, const int* nseq, const int* len, long* off) {
+  const int nk = fused_nk(hd);
   long tot = 0;
   for (int g = 0; g < MAXG; ++g) {
     if (off) off[g] = tot;
-    if (g < ngroups) tot += (long)nseq[g] * H * len[g] * (((long)len[g] + 7) & ~7L);
+    if (g < ngroups && nk) tot += (long)nseq[g] * H * ((len[g] + nk - 1) / nk) * (long)len[g] * hd;
   }
   return tot;
 }
 
-extern "C" int vj_attn_bwd_ds_bytes(int H, int ngroups, const int* nseq, const int* len, long* bytes) {
-  VJ_CHECK_ARG(bytes && nseq && len && ngroups >= 1 && ngroups <= MAXG, "vj_attn_bwd_ds_bytes: bad arguments");
-  *bytes = 2 * ds_elems(H, ngroups, nseq, len, nullptr);
+extern "C" int vj_attn_bwd_ws_bytes(int H, int hd, int ngroups, const int* nseq, const int* len, long* bytes) {
+  VJ_CHECK_ARG(bytes && nseq && len && ngroups >= 1 && ngroups <= MAXG, "vj_attn_bwd_ws_bytes: bad arguments");
+  *bytes = 4 * part_elems(H, hd, ngroups, nseq, len, nullptr);
   return VJ_OK;
 }
 
@@ -1001,7 +1114,7 @@ static int attn_bwd_impl(int T, int H, int hd, const void* qkv, long ld, int q_o
                          const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
                          float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
                          int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t, int fblk,
-                         void* ds_ws, long ds_bytes, void* stream);
+                         void* ws, long ws_bytes, void* stream);
 
 extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
                               const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
@@ -1012,23 +1125,23 @@ extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, in
                        nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, fblk, nullptr, 0, stream);
 }
 
-// As vj_attn_bwd_fc with a dS^T workspace (vj_attn_bwd_ds_bytes): the dK/dV sweep stores dS^T and the
-// dQ sweep multiplies it by K instead of recomputing S, P and dP (non-causal layouts; fblk > 0 or a
-// NULL / short workspace take the recomputing dQ sweep).
+// As vj_attn_bwd_fc with a workspace of vj_attn_bwd_ws_bytes: head dims 32 / 64 without a frame-causal
+// mask then run the fused backward (dQ partials per key block from the dK/dV sweep + a reduce pass)
+// instead of a separate dQ sweep; other layouts, or a NULL / short workspace, take the two sweeps.
 extern "C" int vj_attn_bwd_ws(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
                               const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
                               long ldd, float scale, int ngroups, const int* nseq, const int* len,
                               const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t,
-                              const float* sin_t, int fblk, void* ds_ws, long ds_bytes, void* stream) {
+                              const float* sin_t, int fblk, void* ws, long ws_bytes, void* stream) {
   return attn_bwd_impl(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
-                       nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, fblk, ds_ws, ds_bytes, stream);
+                       nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, fblk, ws, ws_bytes, stream);
 }
 
 static int attn_bwd_impl(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
                          const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
                          float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
                          int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t, int fblk,
-                         void* ds_ws, long ds_bytes, void* stream) {
+                         void* ws, long ws_bytes, void* stream) {
   if (T == 0) return VJ_OK;
   int rc = check_common(H, hd, ld, ldo);
   if (rc) return rc;
@@ -1059,64 +1172,52 @@ static int attn_bwd_impl(int T, int H, int hd, const void* qkv, long ld, int q_o
   const long nth = (long)T * H;
   const int dblocks = (int)((nth + 255) / 256);
   const dim3 gk(ak.sg.tiles_prefix[MAXG], H), gq(aq.sg.tiles_prefix[MAXG], H);
-  const char* env = getenv("VJ_ATTN_DS");
-  // opt-in (VJ_ATTN_DS=1): measured slower than recomputing dS in the dQ sweep (attention)
-  const bool use_ds = ds_ws && fblk == 0 && env && env[0] == '1' &&
-                      ds_bytes >= 2 * ds_elems(H, ngroups, nseq, len, nullptr) && ((uintptr_t)ds_ws & 15) == 0;
-  if (use_ds) {  // dK/dV sweep storing dS^T, then dQ = scale * dS K over it
-    ak.ds = (bf16_t*)ds_ws;
-    ds_elems(H, ngroups, nseq, len, ak.sg.ds_off);
-    AttnArgs ad = a;
-    ad.ds = ak.ds;
-    rc = fill_groups(ad.sg, ngroups, nseq, len, 128, T);
-    if (rc) return rc;
-    ds_elems(H, ngroups, nseq, len, ad.sg.ds_off);
-    const dim3 gd(ad.sg.tiles_prefix[MAXG], H);
-    switch (hd) {
-      case 64:
-        hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
-        hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64>), gk, dim3(256), 0, st, ak);
-        hipLaunchKernelGGL(k_attn_bwd_dq_ds<64>, gd, dim3(256), 0, st, ad);
-        break;
-      case 32:
-        hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
-        hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32>), gk, dim3(256), 0, st, ak);
-        hipLaunchKernelGGL(k_attn_bwd_dq_ds<32>, gd, dim3(256), 0, st, ad);
-        break;
-      case 80:
-        hipLaunchKernelGGL(k_attn_delta<80>, dim3(dblocks), dim3(256), 0, st, a);
-        hipLaunchKernelGGL((k_attn_bwd_dkdv<80, 1>), gk, dim3(256), 0, st, ak);
-        hipLaunchKernelGGL(k_attn_bwd_dq_ds<80>, gd, dim3(256), 0, st, ad);
-        break;
-      default:
-        hipLaunchKernelGGL(k_attn_delta<88>, dim3(dblocks), dim3(256), 0, st, a);
-        hipLaunchKernelGGL((k_attn_bwd_dkdv<88, 1>), gk, dim3(256), 0, st, ak);
-        hipLaunchKernelGGL(k_attn_bwd_dq_ds<88>, gd, dim3(256), 0, st, ad);
-        break;
+  // fused backward, opt-in (VJ_ATTN_FUSED=1): delta, dK/dV + dQ partials, dQ reduce. Measured slower
+  // than the two sweeps (attention backward), so the default stays the two sweeps.
+  const char* fenv = getenv("VJ_ATTN_FUSED");
+  const bool fused = ws && fblk == 0 && fused_nk(hd) > 0 && fenv && fenv[0] == '1' &&
+                     ws_bytes >= 4 * part_elems(H, hd, ngroups, nseq, len, nullptr) && ((uintptr_t)ws & 15) == 0;
+  if (fused) {
+    ak.dqp = (float*)ws;
+    part_elems(H, hd, ngroups, nseq, len, ak.sg.part_off);
+    const long nr = (long)T * H * (hd / 4);
+    const dim3 gr((unsigned)((nr + 255) / 256));
+    if (hd == 64) {
+      hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64, true>), gk, dim3(256), 0, st, ak);
+      hipLaunchKernelGGL((k_attn_dq_reduce<64, 128 * VJ_ATTN_KW64>), gr, dim3(256), 0, st, ak);
+    } else {
+      hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32, true>), gk, dim3(256), 0, st, ak);
+      hipLaunchKernelGGL((k_attn_dq_reduce<32, 128 * VJ_ATTN_KW32>), gr, dim3(256), 0, st, ak);
     }
     VJ_LAUNCH_CHECK("vj_attn_bwd");
     return VJ_OK;
   }
+  // dQ sweep first: it writes -delta for the dK/dV sweep (VJ_ATTN_DELTA=1: the separate delta kernel)
+  const char* denv = getenv("VJ_ATTN_DELTA");
+  const bool sep = denv && denv[0] == '1';
+  aq.dq_delta = sep ? 0 : 1;
   switch (hd) {
     case 64:
-      hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64>), gk, dim3(256), 0, st, ak);
+      if (sep) hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
       hipLaunchKernelGGL((k_attn_bwd_dq<64, VJ_ATTN_QW64>), gq, dim3(256), 0, st, aq);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64>), gk, dim3(256), 0, st, ak);
       break;
     case 32:
-      hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32>), gk, dim3(256), 0, st, ak);
+      if (sep) hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
       hipLaunchKernelGGL((k_attn_bwd_dq<32, VJ_ATTN_QW32>), gq, dim3(256), 0, st, aq);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32>), gk, dim3(256), 0, st, ak);
       break;
     case 80:
-      hipLaunchKernelGGL(k_attn_delta<80>, dim3(dblocks), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<80, 1>), gk, dim3(256), 0, st, ak);
+      if (sep) hipLaunchKernelGGL(k_attn_delta<80>, dim3(dblocks), dim3(256), 0, st, a);
       hipLaunchKernelGGL((k_attn_bwd_dq<80, 1>), gq, dim3(256), 0, st, aq);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<80, 1>), gk, dim3(256), 0, st, ak);
       break;
     default:
-      hipLaunchKernelGGL(k_attn_delta<88>, dim3(dblocks), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<88, 1>), gk, dim3(256), 0, st, ak);
+      if (sep) hipLaunchKernelGGL(k_attn_delta<88>, dim3(dblocks), dim3(256), 0, st, a);
       hipLaunchKernelGGL((k_attn_bwd_dq<88, 1>), gq, dim3(256), 0, st, aq);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<88, 1>), gk, dim3(256), 0, st, ak);
       break;
   }
   VJ_LAUNCH_CHECK("vj_attn_bwd");

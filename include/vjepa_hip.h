@@ -192,6 +192,11 @@ int vj_cast_bf16(long n, const float* in, void* out, void* stream);
 /* dst[c][r] = src[r][c] (bf16; rows, cols, strides multiples of 8): the K-major copy W^T that the
  * data-gradient GEMM dX = dY W (nn.Linear backward) reads as its B operand. */
 int vj_transpose_bf16(int rows, int cols, const void* src, long ld_src, void* dst, long ld_dst, void* stream);
+/* n bf16 transposes in one launch (the per-step W^T copies): desc = DEVICE int64 [n][8] =
+ * {src, dst, rows, cols, ld_src, ld_dst, first_tile, tiles_x} with 64 x 64 tiles numbered
+ * consecutively (first_tile = running sum of ceil(rows/64)*ceil(cols/64), tiles_x = ceil(cols/64));
+ * each matrix meets vj_transpose_bf16's constraints. Replaces one vj_transpose_bf16 launch per weight. */
+int vj_transpose_bf16_batch(int n, const long* desc, long total_tiles, void* stream);
 
 /* JEPA multi-block 3-D masks on the device (src/masks/multiseq_multiblock3d.py:155-239): the host
  * makes the reference's RNG draws (block size, (start, top, left) per block: boxes int32

@@ -429,6 +429,9 @@ def test_fused_rope_paths(M, hd, H, monkeypatch):
             monkeypatch.setenv("VJ_GEMM_PP", pp)
             other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
             assert torch.equal(fused, other), f"qkv_rope: VJ_GEMM_PP={pp} differs from the default kernel"
+        monkeypatch.setenv("VJ_GEMM_PP", "2")  # 32x32x16 form: other K order, one bf16 rounding apart
+        other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
+        _close(other, fused, 1e-3, 8e-3, "qkv_rope VJ_GEMM_PP=2 vs default")
         if prev is None:
             monkeypatch.delenv("VJ_GEMM_PP")
         else:
@@ -676,3 +679,57 @@ def test_gemm_pingpong_matches_one_tile_kernel(K, pxcd, monkeypatch):
         _close(pp["bf16"], ref, 1e-3, 8e-3, "pp EPI_BF16")
         assert torch.equal(pp["gelu_a"], pp["gelu_nosave"])
         _close(pp["gelu_bwd"], (X.float() @ W.float().t()) * dgs.float(), 2e-3, 1.5e-2, "pp EPI_GELU_BWD")
+        # the 32x32x16 form (VJ_GEMM_PP=2): another K summation order inside each MFMA, so f32 outputs
+        # agree with the one-tile kernel to accumulation rounding and bf16 outputs to one rounding step
+        monkeypatch.setenv("VJ_GEMM_PP", "2")
+        p32 = run()
+        monkeypatch.delenv("VJ_GEMM_PP")
+        tol32 = 2e-6 * math.sqrt(K) * float(ref.abs().max())
+        for k in ("f32", "f32_resid"):
+            _close(p32[k], one[k], tol32, 1e-5, f"pp32 {k} vs one-tile")
+        for k in ("bf16", "bf16_resid", "gelu_a", "gelu_d", "gelu_bwd"):
+            _close(p32[k], one[k], 1e-3, 8e-3, f"pp32 {k} vs one-tile")
+            frac = (p32[k] != one[k]).float().mean().item()
+            assert frac < 0.05, f"pp32 {k}: {frac:.3f} of the bf16 outputs differ from the one-tile kernel"
+        assert torch.equal(p32["gelu_a"], p32["gelu_nosave"])
+        _close(p32["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "pp32 EPI_F32 vs fp32")
+
+
+def test_transpose_bf16_single_and_batched():
+    """Register-tile transpose (8 x 8 blocks per lane, one 64 x 64 tile per wave) and its batched
+    form (one launch over a descriptor table, as refresh_weight_transposes uses): bitwise x.t(), on
+    shapes with ragged 64-tiles, row-strided sources and the ViT-L / predictor weight shapes."""
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(7)
+    shapes = [(8, 8), (72, 136), (3072, 1024), (1024, 4096), (384, 1536), (1152, 384), (200, 64)]
+    srcs = [torch.randn(r, c, generator=g).to(DEV).bfloat16() for r, c in shapes]
+    big = torch.randn(96, 200, generator=g).to(DEV).bfloat16()
+    srcs.append(big[:, 8:136])  # row stride 200 > cols
+    for x in srcs:
+        assert torch.equal(ops.transpose_bf16(x), x.t().contiguous()), tuple(x.shape)
+    outs = [torch.full((x.shape[1], x.shape[0]), 7.0, device=DEV, dtype=torch.bfloat16) for x in srcs]
+    desc, tiles = ops.transpose_batch_desc(list(zip(srcs, outs)))
+    ops.transpose_bf16_batch(desc, len(srcs), tiles)
+    torch.cuda.synchronize()
+    for x, o in zip(srcs, outs):
+        assert torch.equal(o, x.t().contiguous()), tuple(x.shape)
+
+
+def test_refresh_weight_transposes_matches_lazy_copies():
+    """After an arena update the batched refresh leaves every registered W^T equal to the transpose
+    of the new bf16 shadow, and weight_bf16_t then returns it without a new launch."""
+    from vjepa2_amd import functions as F
+
+    lin = torch.nn.Linear(256, 384).to(DEV)
+    w = lin.weight
+    w._vj_bf16 = w.detach().bfloat16()
+    first = F.weight_bf16_t(w)
+    assert torch.equal(first, w._vj_bf16.t().contiguous())
+    w._vj_bf16.copy_((w.detach() * 2).bfloat16())  # an "AdamW" update of the shadow
+    F.SHADOW_EPOCH[0] += 1
+    F.refresh_weight_transposes()
+    torch.cuda.synchronize()
+    assert w._vj_bf16_t[0][1] == F.SHADOW_EPOCH[0]
+    assert torch.equal(w._vj_bf16_t[1], w._vj_bf16.t().contiguous())
+    assert F.weight_bf16_t(w) is w._vj_bf16_t[1]

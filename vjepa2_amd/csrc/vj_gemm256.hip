@@ -888,10 +888,10 @@ int launch256(int epi, const G256& g, hipStream_t st) {
 
 }  // namespace
 
-bool vj_gemm_pp_enabled(int epi);
+int vj_gemm_pp_mode(int epi);
 int vj_gemm_pp_dispatch(int M, int N, int K, const void* A, long lda, const void* B, long ldb, int epi,
                         const float* bias, const void* aux, long ldaux, void* C, long ldc, void* C2, long ldc2,
-                        hipStream_t st, const void* rope, int group, int grid);
+                        hipStream_t st, const void* rope, int group, int grid, int mode);
 
 // Called by vj_gemm_bf16_splitk (splitk == 1) when the problem suits a 256-row tile; arguments
 // already validated there. Returns VJ_ERR_UNSUPPORTED when it declines.
@@ -903,10 +903,11 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
   if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
     return VJ_ERR_UNSUPPORTED;
   // K-major A and B: the ping-pong kernel (vj_gemm_pp.hip) when it takes the shape
-  if (a_kmajor && b_kmajor && vj_gemm_pp_enabled(epi)) {
+  const int ppm = a_kmajor && b_kmajor ? vj_gemm_pp_mode(epi) : 0;
+  if (ppm) {
     const int tm = vj_cdiv(M, 256), tn = vj_cdiv(N, 128);
     const int rc = vj_gemm_pp_dispatch(M, N, K, A, lda, B, ldb, epi, bias, aux, ldaux, C, ldc, C2, ldc2, st, rope,
-                                       tile_group(tm, tn), grid256((long)tm * tn));
+                                       tile_group(tm, tn), grid256((long)tm * tn), ppm);
     if (rc != VJ_ERR_UNSUPPORTED) return rc;
   }
   // 256-wide tiles (direct-store epilogue) unless the last column tile would waste > 15 % of the work

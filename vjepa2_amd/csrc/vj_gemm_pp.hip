@@ -22,6 +22,15 @@
 // under the current phase's MFMAs), and B is staged row-permuted so each lane owns 4 consecutive
 // output columns and the epilogue stores straight from registers.
 //
+// M32 = true: the same pipeline on v_mfma_f32_32x32x16_bf16. One 32x32x16 MFMA holds its SIMD's
+// vector-issue port for 8 of its 32 cycles (the 16x16x32 form: 8 of 16), so the epilogue group gets
+// three times the issue slots per flop. Per wave the tile is 64 x 128 (2 x 4 accumulator blocks of
+// 32 x 32, the 4 waves of a group stacked in M), B is staged with a 32-row permutation (LDS row r of
+// the 128-row tile holds global row 4 (r % 32) + r / 32, so lane l again owns 4 consecutive output
+// columns 4 (l & 31) .. + 3), and each K-tile's 12 DMA pieces are spread over four phases (3 per
+// phase: the 8 MFMAs of a phase cannot cover 12 pieces' issue) — pieces 0-2 of K-tile b + 3 after
+// barrier b, pieces 3-11 in the three phases before barrier b + 1, so the vmcnt(12) count is unchanged.
+//
 // Requirements (host-checked, else the caller falls back): A and B K-major, K % 64 == 0 (no K-tail:
 // DMA offsets are per-lane constants plus a scalar k offset), K >= 192 (a tile has at least as many
 // K-tiles as the ring has stages), N % 8 == 0, 16-B aligned pointers.
@@ -45,9 +54,11 @@ __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, LDS_AS void* ld
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_wave_base, 16, voff, soff, 0, 0);
 }
 
-template <int EPI>
+template <int EPI, bool M32>
 __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
-  constexpr int BM = 256, BN = 128, NTN = 4, WN = 64;
+  constexpr int BM = 256, BN = 128, NTN = 4;
+  constexpr int WN = M32 ? 128 : 64;  // wave tile columns (M32: one wave column, 4 wave rows of 64)
+  constexpr int WM = M32 ? 64 : 128;  // wave tile rows
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr bool AUX = EPI == EPI_F32_RESID || EPI == EPI_GELU_BWD || EPI == EPI_BF16_RESID;
   constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_F32_RESID;
@@ -59,7 +70,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = wave >> 2, w4 = wave & 3, wr = w4 >> 1, wc = w4 & 1;
+  const int grp = wave >> 2, w4 = wave & 3, wr = M32 ? w4 : w4 >> 1, wc = M32 ? 0 : w4 & 1;
 
   // Persistent walk (as k_gemm256): the logical tiles are cut into 8 runs, one per XCD; the P
   // blocks of an XCD walk its run with stride P. This block's tiles: first, first + P, ...
@@ -108,8 +119,13 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
       const int ca = (lane & 7) ^ ((ra >> 1) & 7);
       aoff[e] = (uint32_t)(ra * g.lda * 2 + ca * 16);
       const int rb = w4 * 32 + e * 8 + r8;  // LDS row
-      const int rl = rb % WN;
-      const int gr = (rb - rl) + NTN * (rl & 15) + (rl >> 4);
+      int gr;
+      if constexpr (M32) {  // LDS row r -> global row 4 (r % 32) + r / 32 (the whole 128-row tile)
+        gr = 4 * (rb & 31) + (rb >> 5);
+      } else {
+        const int rl = rb % WN;
+        gr = (rb - rl) + NTN * (rl & 15) + (rl >> 4);
+      }
       const int cb = (lane & 7) ^ ((rb >> 1) & 7);
       boff[e] = (uint32_t)(gr * g.ldb * 2 + cb * 16);
     }
@@ -123,15 +139,24 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
   // One K-tile (k offset kb bytes) -> LDS slot `slot`, issued by the calling group's 4 waves;
   // kill = VJ_OOB makes every piece out of range (zero-fill dummies past the block's last K-tile,
   // so every K-tile issues the same number of pieces and the vmcnt counts stay constant)
-  auto dma_issue = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int kb, uint32_t kill, int slot) {
+  // Piece q (0-7: A, 8-11: B) of one K-tile: A rows (w4 * 8 + q) * 8 .. + 7 = base + 16 (q >> 1)
+  // rows; B LDS rows (w4 * 4 + i) * 8 .. + 7 (global rows permuted): piece i & 1 shifted by the
+  // permutation's row step (16-wide: 1 global row per 16 LDS rows; M32: 64 global rows per 16)
+  constexpr int BSTEP = M32 ? 64 : 1;
+  auto dma_piece = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int kb, uint32_t kill, LDS_AS char* s,
+                       int q) {
+    if (q < 8)
+      dma16s(ra, s + (w4 * 8 + q) * 1024, (aoff[q & 1] + (uint32_t)((q >> 1) * 16 * g.lda * 2)) | kill, kb);
+    else
+      dma16s(rb, s + A_BYTES + (w4 * 4 + (q - 8)) * 1024,
+             (boff[q & 1] + (uint32_t)(((q - 8) >> 1) * BSTEP * g.ldb * 2)) | kill, kb);
+  };
+  auto dma_issue = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int kb, uint32_t kill, int slot,
+                       int q0 = 0, int q1 = DMA_PIECES) {
     LDS_AS char* s = smem + slot * STAGE;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)  // A rows (w4 * 8 + i) * 8 .. + 7: i-th piece = base + 16 i rows
-      dma16s(ra, s + (w4 * 8 + i) * 1024, (aoff[i & 1] + (uint32_t)((i >> 1) * 16 * g.lda * 2)) | kill, kb);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)  // B LDS rows (w4 * 4 + i) * 8 .. + 7 (global rows permuted): piece
-      // i = piece i & 1 shifted by i >> 1 global rows (the permutation's row step)
-      dma16s(rb, s + A_BYTES + (w4 * 4 + i) * 1024, (boff[i & 1] + (uint32_t)((i >> 1) * g.ldb * 2)) | kill, kb);
+    for (int q = 0; q < DMA_PIECES; ++q)
+      if (q >= q0 && q < q1) dma_piece(ra, rb, kb, kill, s, q);
   };
 
   // RoPE tables: interleaved cos/sin (read once per workgroup) behind the per-wave row positions
@@ -152,16 +177,24 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
       if (e < ntab) rtab[e] = rpf[i];
     }
   }
-  if (grp == 0) {  // the first NST K-tiles (all of tile 0: nk >= NST)
+  if (grp == 0) {  // the first NST K-tiles (all of tile 0: nk >= NST); M32: of K-tile 2 only the
+    // pieces 0-2 (its pieces 3-11 are issued in K-tile 0's phases 0-2)
     __amdgpu_buffer_rsrc_t ra, rb;
     tile_rsrc(0, ra, rb);
-    for (int v = 0; v < NST; ++v) dma_issue(ra, rb, v * BK * 2, 0u, v);
+    for (int v = 0; v < NST; ++v) dma_issue(ra, rb, v * BK * 2, 0u, v, 0, M32 && v == NST - 1 ? 3 : DMA_PIECES);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  f32x4 acc[8][NTN];
+  [[maybe_unused]] f32x4 acc[8][NTN];
+  [[maybe_unused]] f32x16 acc32[2][NTN];  // M32: [m-block][n-block], 32 x 32 each
   bf16x8 Aa[4], Ab[4], Ba[NTN], Bb[NTN];
+  // accumulator of row group i (4 rows: 16-wide m-tile i; M32: m-block i >> 2, register quad i & 3),
+  // n-tile j, row r of the group
+  auto accv = [&](int i, int j, int r) -> float {
+    if constexpr (M32) return acc32[i >> 2][j][4 * (i & 3) + r];
+    else return acc[i][j][r];
+  };
   // Fragment reads (the K-major frag() of vj_gemm_tile.h, written out): every fragment row block
   // starts at a multiple of 16 rows, so the XOR swizzle depends on the lane only and a read is
   // slot base + wave base + lane offset (one VGPR per k-step) + a compile-time immediate. Three
@@ -263,11 +296,94 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
         phase(Ab, 1, Bb, [&](int q) {
           if (q < 4) rdA1(Aa, q, sn, 0, 0);
           else if (q < 8) rdB1(Ba, q - 4, sn, 0);
-          if (q < 8)  // A rows (w4 * 8 + q) * 8 .. + 7: piece q = base + 16 (q >> 1) rows
-            dma16s(ra, st + (w4 * 8 + q) * 1024, (aoff[q & 1] + (uint32_t)((q >> 1) * 16 * g.lda * 2)) | kill, kb);
-          else if (q < 12)  // B LDS rows (w4 * 4 + i) * 8 .. + 7: global rows of piece i & 1 + (i >> 1)
-            dma16s(rb, st + A_BYTES + (w4 * 4 + (q - 8)) * 1024,
-                   (boff[q & 1] + (uint32_t)(((q - 8) >> 1) * g.ldb * 2)) | kill, kb);
+          if (q < DMA_PIECES) dma_piece(ra, rb, kb, kill, st, q);
+        });
+      }
+      sl = sn;
+    }
+#if VJ_PP_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+  };
+
+  // ---- M32: 32x32x16 fragments. Lane l reads row (l & 31) of a 32-row block, 16-B chunk
+  // 2 ks + (l >> 5) of k-step ks (16 deep); the K-major swizzle (chunk ^= (row >> 1) & 7) keeps every
+  // 16-lane quarter on 16 distinct bank slots. A: the wave's 2 m-blocks (rows wr * 64 + 32 i), B: the
+  // tile's 4 n-blocks (LDS rows 32 j, permuted at staging).
+  [[maybe_unused]] uint32_t loff32[4];
+  if constexpr (M32) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      loff32[ks] = (lane & 31) * 128 + (((2 * ks + (lane >> 5)) ^ (((lane & 31) >> 1) & 7)) * 16);
+  }
+  // fragment q of a k-step: q < 2 A m-block q (into X), else B n-block q - 2 (into Y)
+  auto rd32 = [&](bf16x8 (&X)[4], bf16x8 (&Y)[NTN], int q, int slot, int ks) {
+    const uint32_t base = lds0 + slot * STAGE + loff32[ks];
+    if (q < 2) X[q] = *(const LDS_AS bf16x8*)((const LDS_AS char*)(uintptr_t)(base + wr * 64 * 128) + q * 32 * 128);
+    else Y[q - 2] = *(const LDS_AS bf16x8*)((const LDS_AS char*)(uintptr_t)(base + A_BYTES) + (q - 2) * 32 * 128);
+  };
+  // one k-step = 8 MFMAs (2 m-blocks x 4 n-blocks), each followed by side(q)
+  auto phase32 = [&](const bf16x8 (&X)[4], const bf16x8 (&Y)[NTN], auto&& side) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      acc32[q >> 2][q & 3] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[q >> 2], Y[q & 3], acc32[q >> 2][q & 3], 0, 0, 0);
+      side(q);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // The M32 K-loop of tile p. In K-tile iteration b = u0 + t: phases 0-2 (k-steps 0-2) issue pieces
+  // 3-11 of K-tile b + 2 (into its slot, freed at barrier b - 1), phase 3 (after barrier b) pieces
+  // 0-2 of K-tile b + 3 (into slot b, just freed). K-tile b + 2 is then complete before the wait
+  // ahead of barrier b + 1, whose vmcnt(12) leaves exactly its 12 pieces in flight. A group's first
+  // K-tile continues the K-tile b + 2 the other group started in its last phase 3.
+  auto kloop32 = [&](int u0, int p) {
+    __amdgpu_buffer_rsrc_t raC, rbC, raN, rbN;
+    tile_rsrc(p, raC, rbC);
+    tile_rsrc(p + 1, raN, rbN);
+    const uint32_t killN = p + 1 < ntl ? 0u : VJ_OOB;
+#if VJ_PP_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NTN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc32[i][j][e] = 0.f;
+    int sl = u0 % NST;  // slot of K-tile u0 + t
+#pragma unroll
+    for (int q = 0; q < 6; ++q) rd32(Aa, Ba, q, sl, 0);
+    for (int t = 0; t < nk; ++t) {
+      const int sn = sl + 1 == NST ? 0 : sl + 1;
+      const int sp = sn + 1 == NST ? 0 : sn + 1;  // slot of K-tile b + 2 (= b - 1)
+      {  // pieces 3-11 of K-tile b + 2: three per phase, in the gaps after MFMAs 1, 4, 7
+        const int td = t + 2;
+        const bool own = td < nk;
+        const __amdgpu_buffer_rsrc_t ra = own ? raC : raN, rb = own ? rbC : rbN;
+        const int kb = (own ? td : td - nk) * BK * 2;
+        const uint32_t kill = own ? 0u : killN;
+        LDS_AS char* st = smem + sp * STAGE;
+        auto dq = [&](int ph, int q) {
+          if (q == 1 || q == 4 || q == 7) dma_piece(ra, rb, kb, kill, st, 3 + 3 * ph + (q == 1 ? 0 : q == 4 ? 1 : 2));
+        };
+        phase32(Aa, Ba, [&](int q) { if (q < 6) rd32(Ab, Bb, q, sl, 1); dq(0, q); });
+        phase32(Ab, Bb, [&](int q) { if (q < 6) rd32(Aa, Ba, q, sl, 2); dq(1, q); });
+        phase32(Aa, Ba, [&](int q) { if (q < 6) rd32(Ab, Bb, q, sl, 3); dq(2, q); });
+      }
+      static_assert(NST == 3 && DMA_PIECES == 12, "vmcnt count written for 3 stages x 12 pieces");
+      asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      {  // phase 3: k-step 3, the next K-tile's k-step-0 fragments, pieces 0-2 of K-tile b + 3
+        const int td = t + NST;
+        const bool own = td < nk;
+        const __amdgpu_buffer_rsrc_t ra = own ? raC : raN, rb = own ? rbC : rbN;
+        const int kb = (own ? td : td - nk) * BK * 2;
+        const uint32_t kill = own ? 0u : killN;
+        LDS_AS char* st = smem + sl * STAGE;
+        phase32(Ab, Bb, [&](int q) {
+          if (q < 6) rd32(Aa, Ba, q, sn, 0);
+          if (q == 1 || q == 4 || q == 7) dma_piece(ra, rb, kb, kill, st, q == 1 ? 0 : q == 4 ? 1 : 2);
         });
       }
       sl = sn;
@@ -294,9 +410,13 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
         ++done;
       }
     };
-    const int nb = cur.n0 + wc * WN + NTN * (lane & 15);
+    // lane's 4 columns nb .. nb + 3; row r of row group i: mb + rofs(i) + r (16-wide: m-tile i, rows
+    // 4 (lane >> 4) + r; M32: m-block i >> 2, rows 8 (i & 3) + 4 (lane >> 5) + r of the block)
+    const int nb = cur.n0 + wc * WN + NTN * (lane & (M32 ? 31 : 15));
     const bool nok = nb < g.N;
-    const int mb = cur.m0 + wr * 128 + 4 * (lane >> 4);
+    const int mrow = M32 ? 4 * (lane >> 5) : 4 * (lane >> 4);  // row of the lane within a row group
+    const int mb = cur.m0 + wr * WM + mrow;
+    auto rofs = [](int i) { return M32 ? (i >> 2) * 32 + (i & 3) * 8 : i * 16; };
     float bias[NTN];
 #pragma unroll
     for (int j = 0; j < NTN; ++j) bias[j] = 0.f;
@@ -307,10 +427,10 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
     [[maybe_unused]] int rsh[NTN / 2], rf0[NTN / 2], rf1[NTN / 2];
     if constexpr (EPI == EPI_ROPE) {
       const VjRope& r = g.rope;
-      // this wave's 128 rows: (frame | row << 10 | col << 20), wave-private LDS
+      // this wave's WM rows: (frame | row << 10 | col << 20), wave-private LDS
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int m = cur.m0 + wr * 128 + lane + 64 * h;
+      for (int h = 0; h < WM / 64; ++h) {
+        const int m = cur.m0 + wr * WM + lane + 64 * h;
         int id = 0;
         if (m < g.M) id = r.ids ? r.ids[m] : m % r.mod;
         const int fr = id / r.tpf, rem = id - r.tpf * fr, hr = rem / r.tpr;
@@ -332,7 +452,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
     auto fetch = [&](int i, float (&dst)[4][NTN]) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = mb + i * 16 + r;
+        const int m = mb + rofs(i) + r;
         const bool ok = m < g.M && nok;
         const long off = ok ? (long)m * g.ldaux + nb : 0;
         if constexpr (EPI == EPI_F32_RESID) {
@@ -359,7 +479,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int r = odd ? 2 + h : h;
-        const int m = mb + i * 16 + r;
+        const int m = mb + rofs(i) + r;
         if (m < g.M && nok8) {
           const uint4 v = odd ? make_uint4(rcv[2 * h], rcv[2 * h + 1], pk[r][0], pk[r][1])
                               : make_uint4(pk[r][0], pk[r][1], rcv[2 * h], rcv[2 * h + 1]);
@@ -380,11 +500,11 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
         if constexpr (F32OUT) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int m = mb + i * 16 + r;
+            const int m = mb + rofs(i) + r;
             float v[NTN];
 #pragma unroll
             for (int j = 0; j < NTN; ++j) {
-              v[j] = acc[i][j][r] + bias[j];
+              v[j] = accv(i, j, r) + bias[j];
               if constexpr (EPI == EPI_F32_RESID) v[j] += aux[i % (AUX_PF + 1)][r][j];
             }
             if (m < g.M && nok) *(float4*)((float*)g.C + (long)m * g.ldc + nb) = make_float4(v[0], v[1], v[2], v[3]);
@@ -395,9 +515,9 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
           for (int r = 0; r < 4; ++r) {
             float v[NTN];
 #pragma unroll
-            for (int j = 0; j < NTN; ++j) v[j] = acc[i][j][r] + bias[j];
+            for (int j = 0; j < NTN; ++j) v[j] = accv(i, j, r) + bias[j];
             if constexpr (EPI == EPI_ROPE) {
-              const int rp = rposw[i * 16 + 4 * (lane >> 4) + r];
+              const int rp = rposw[rofs(i) + mrow + r];
 #pragma unroll
               for (int p = 0; p < NTN / 2; ++p) {
                 if (!ract[p]) continue;
@@ -444,7 +564,8 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
   int u0 = 0;
   for (int p = 0; p < ntl; ++p, u0 += nk) {
     if ((p & 1) == grp) {
-      kloop(u0, p);
+      if constexpr (M32) kloop32(u0, p);
+      else kloop(u0, p);
     } else if (p == 0) {
       for (int b = 0; b < nk; ++b) __builtin_amdgcn_s_barrier();
     } else {
@@ -458,6 +579,12 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
   if (((ntl - 1) & 1) == grp) epilogue(make_tile(ntl - 1), 0);
 }
 
+template <int EPI>
+void launch_pp(bool m32, dim3 gr, hipStream_t st, const G256& g) {
+  if (m32) hipLaunchKernelGGL((k_gemm_pp<EPI, true>), gr, dim3(512), 0, st, g);
+  else hipLaunchKernelGGL((k_gemm_pp<EPI, false>), gr, dim3(512), 0, st, g);
+}
+
 }  // namespace
 
 // Which K-major GEMMs come here: VJ_GEMM_PP=0 none, =1 all, unset: the epilogues in the bit mask
@@ -466,20 +593,22 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
 // target QKV and every other epilogue (the lone-wave K-loop runs at ~0.9 of the two-wave one and
 // the epilogues do not fully hide under it); the step measured 192.2 clips/s with the RoPE shapes
 // routed here vs 193.4 without (bench.py A/B in one call), so the default stays k_gemm256.
-bool vj_gemm_pp_enabled(int epi) {
+// VJ_GEMM_PP=2 (or the epilogue's bit in VJ_GEMM_PP32_EPIS) selects the M32 (32x32x16) form.
+// Returns 0 (k_gemm256), 1 (ping-pong, 16x16x32) or 2 (ping-pong, 32x32x16).
+int vj_gemm_pp_mode(int epi) {
   const char* e = getenv("VJ_GEMM_PP");
-  if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
+  if (e && (e[0] == '0' || e[0] == '1' || e[0] == '2')) return e[0] - '0';
+  const char* m2 = getenv("VJ_GEMM_PP32_EPIS");
+  if (m2 && ((strtol(m2, nullptr, 0) >> epi) & 1)) return 2;
   const char* m = getenv("VJ_GEMM_PP_EPIS");
-  const long mask = m ? strtol(m, nullptr, 0) : 0L;
-  return (mask >> epi) & 1;
+  return (m && ((strtol(m, nullptr, 0) >> epi) & 1)) ? 1 : 0;
 }
 
 // Called by vj_gemm256_dispatch for K-major A and B; VJ_ERR_UNSUPPORTED when the shape is not one
 // this kernel takes (the caller then uses k_gemm256).
 int vj_gemm_pp_dispatch(int M, int N, int K, const void* A, long lda, const void* B, long ldb, int epi,
                         const float* bias, const void* aux, long ldaux, void* C, long ldc, void* C2, long ldc2,
-                        hipStream_t st, const void* rope, int group, int grid) {
+                        hipStream_t st, const void* rope, int group, int grid, int mode) {
   if (K % BK || K < NST * BK || N % 8) return VJ_ERR_UNSUPPORTED;  // whole K-tiles, nk >= NST
   if (epi == EPI_PARTIAL || epi < EPI_BF16 || (epi > EPI_ROPE && epi != EPI_BF16_RESID)) return VJ_ERR_UNSUPPORTED;
   if ((long)(M + 255) * lda * 2 > 0x7fffffffL || (long)(N + 127) * ldb * 2 > 0x7fffffffL) return VJ_ERR_UNSUPPORTED;
@@ -491,15 +620,16 @@ int vj_gemm_pp_dispatch(int M, int N, int K, const void* A, long lda, const void
     g.rope = *(const VjRope*)rope;
     if ((long)g.rope.npos * g.rope.half > PP_ROPE_TAB_MAX) return VJ_ERR_UNSUPPORTED;
   }
-  const dim3 gr(grid), blk(512);
+  const dim3 gr(grid);
+  const bool m32 = mode == 2;
   switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL(k_gemm_pp<EPI_BF16>, gr, blk, 0, st, g); break;
-    case EPI_F32: hipLaunchKernelGGL(k_gemm_pp<EPI_F32>, gr, blk, 0, st, g); break;
-    case EPI_F32_RESID: hipLaunchKernelGGL(k_gemm_pp<EPI_F32_RESID>, gr, blk, 0, st, g); break;
-    case EPI_GELU: hipLaunchKernelGGL(k_gemm_pp<EPI_GELU>, gr, blk, 0, st, g); break;
-    case EPI_GELU_BWD: hipLaunchKernelGGL(k_gemm_pp<EPI_GELU_BWD>, gr, blk, 0, st, g); break;
-    case EPI_ROPE: hipLaunchKernelGGL(k_gemm_pp<EPI_ROPE>, gr, blk, 0, st, g); break;
-    case EPI_BF16_RESID: hipLaunchKernelGGL(k_gemm_pp<EPI_BF16_RESID>, gr, blk, 0, st, g); break;
+    case EPI_BF16: launch_pp<EPI_BF16>(m32, gr, st, g); break;
+    case EPI_F32: launch_pp<EPI_F32>(m32, gr, st, g); break;
+    case EPI_F32_RESID: launch_pp<EPI_F32_RESID>(m32, gr, st, g); break;
+    case EPI_GELU: launch_pp<EPI_GELU>(m32, gr, st, g); break;
+    case EPI_GELU_BWD: launch_pp<EPI_GELU_BWD>(m32, gr, st, g); break;
+    case EPI_ROPE: launch_pp<EPI_ROPE>(m32, gr, st, g); break;
+    case EPI_BF16_RESID: launch_pp<EPI_BF16_RESID>(m32, gr, st, g); break;
     default: return VJ_ERR_UNSUPPORTED;
   }
   VJ_LAUNCH_CHECK("vj_gemm_pp");

@@ -959,37 +959,65 @@ __global__ void k_cast_bf16(long n4, const float4* __restrict__ in, uint2* __res
   }
 }
 
-// bf16 transpose dst[c][r] = src[r][c] through a 64 x 64 LDS tile (16-B loads and stores): the
-// K-major copy W^T of a weight that the data-gradient GEMM dX = dY W reads (direct-store epilogue).
-__global__ __launch_bounds__(256) void k_transpose_bf16(int rows, int cols, const bf16_t* __restrict__ src, long lds_,
-                                                        bf16_t* __restrict__ dst, long ldd) {
-  __shared__ bf16_t t[64][64 + 2];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
-  const int tr = threadIdx.x >> 3, tc = (threadIdx.x & 7) * 8;  // 32 rows x 8 chunks of 8 per pass
+// 8 x 8 bf16 block transpose in registers: a[j] = row j (8 bf16 in 4 dwords) -> b[i] = column i.
+// b[i] dword k = (a[2k][i], a[2k+1][i]): v_perm_b32 picks the low (i even) or high halves.
+__device__ __forceinline__ void transpose8x8(const uint4 (&a)[8], uint4 (&b)[8]) {
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int r = r0 + tr + 32 * p, c = c0 + tc;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r < rows && c < cols) v = *(const uint4*)(src + (long)r * lds_ + c);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t sel = (i & 1) ? 0x07060302u : 0x05040100u;
+    uint32_t w[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      t[tr + 32 * p][tc + 2 * k] = (bf16_t)(w[k] & 0xffff);
-      t[tr + 32 * p][tc + 2 * k + 1] = (bf16_t)(w[k] >> 16);
+      const uint32_t* lo = (const uint32_t*)&a[2 * k];
+      const uint32_t* hi = (const uint32_t*)&a[2 * k + 1];
+      w[k] = __builtin_amdgcn_perm(hi[i >> 1], lo[i >> 1], sel);
     }
+    b[i] = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  __syncthreads();
+}
+
+// One 64 x 64 tile per wave, no LDS: lane (br = lane >> 3, bc = lane & 7) loads the 8 x 8 block at
+// rows r0 + 8 br .. + 7, columns c0 + 8 bc .. + 7 (8 x 16 B; the 8 lanes of a block row read one
+// 128-B line per row), transposes it in registers and stores rows c0 + 8 bc .. + 7 of dst at columns
+// r0 + 8 br .. + 7 (the 8 lanes of a bc read-out again cover 128 contiguous bytes per row).
+__device__ __forceinline__ void transpose_tile64(const bf16_t* __restrict__ src, long lds_, bf16_t* __restrict__ dst,
+                                                 long ldd, int rows, int cols, int r0, int c0, int lane) {
+  const int r = r0 + 8 * (lane >> 3), c = c0 + 8 * (lane & 7);
+  if (r >= rows || c >= cols) return;  // rows, cols are multiples of 8: a block is whole or absent
+  uint4 a[8], b[8];
 #pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int c = c0 + tr + 32 * p, r = r0 + tc;  // output row c, columns r .. r+7
-    if (c < cols && r < rows) {
-      uint32_t w[4];
+  for (int j = 0; j < 8; ++j) a[j] = *(const uint4*)(src + (long)(r + j) * lds_ + c);
+  transpose8x8(a, b);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        w[k] = (uint32_t)t[tc + 2 * k][tr + 32 * p] | ((uint32_t)t[tc + 2 * k + 1][tr + 32 * p] << 16);
-      *(uint4*)(dst + (long)c * ldd + r) = make_uint4(w[0], w[1], w[2], w[3]);
+  for (int i = 0; i < 8; ++i) *(uint4*)(dst + (long)(c + i) * ldd + r) = b[i];
+}
+
+// Batched transpose of many weights in one launch (the per-step W^T copies of the data-gradient
+// GEMMs): desc[i] = {src, dst, rows, cols, ld_src, ld_dst, first tile, tiles across} (int64 each),
+// tiles of 64 x 64 numbered consecutively over the batch; a wave finds its matrix by binary search.
+__global__ __launch_bounds__(256) void k_transpose_bf16_batch(const long* __restrict__ desc, int n, long total) {
+  const int lane = threadIdx.x & 63;
+  for (long t = (long)blockIdx.x * 4 + (threadIdx.x >> 6); t < total; t += (long)gridDim.x * 4) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {  // last i with desc[i].first <= t
+      const int mid = (lo + hi + 1) >> 1;
+      if (desc[mid * 8 + 6] <= t) lo = mid;
+      else hi = mid - 1;
     }
+    const long* d = desc + lo * 8;
+    const long loc = t - d[6];
+    const int tx = (int)d[7];
+    const int by = (int)(loc / tx), bx = (int)(loc - (long)by * tx);
+    transpose_tile64((const bf16_t*)d[0], d[4], (bf16_t*)d[1], d[5], (int)d[2], (int)d[3], by * 64, bx * 64, lane);
   }
+}
+
+// bf16 transpose dst[c][r] = src[r][c]: 4 waves per block, one 64 x 64 tile per wave (tiles along
+// the columns: block x covers column tiles 4 x .. 4 x + 3)
+__global__ __launch_bounds__(256) void k_transpose_bf16(int rows, int cols, const bf16_t* __restrict__ src, long lds_,
+                                                        bf16_t* __restrict__ dst, long ldd) {
+  const int tx = blockIdx.x * 4 + (threadIdx.x >> 6);
+  transpose_tile64(src, lds_, dst, ldd, rows, cols, blockIdx.y * 64, tx * 64, threadIdx.x & 63);
 }
 
 inline int grid_stride_blocks(long n4) {
@@ -1325,10 +1353,24 @@ extern "C" int vj_transpose_bf16(int rows, int cols, const void* src, long ld_sr
   VJ_CHECK_ARG(rows % 8 == 0 && cols % 8 == 0 && ld_src % 8 == 0 && ld_dst % 8 == 0 && ld_src >= cols &&
                    ld_dst >= rows && !(((uintptr_t)src | (uintptr_t)dst) & 15),
                "vj_transpose_bf16: rows, cols, strides must be multiples of 8 and the pointers 16-B aligned");
-  const dim3 grid(vj_cdiv(cols, 64), vj_cdiv(rows, 64));
+  const dim3 grid(vj_cdiv(vj_cdiv(cols, 64), 4), vj_cdiv(rows, 64));
   hipLaunchKernelGGL(k_transpose_bf16, grid, dim3(256), 0, (hipStream_t)stream, rows, cols, (const bf16_t*)src,
                      ld_src, (bf16_t*)dst, ld_dst);
   VJ_LAUNCH_CHECK("vj_transpose_bf16");
+  return VJ_OK;
+}
+
+// n transposes in one launch. desc: DEVICE array of n x 8 int64 {src, dst, rows, cols, ld_src, ld_dst,
+// first_tile, tiles_x} (first_tile = running sum of ceil(rows/64) * ceil(cols/64); tiles_x =
+// ceil(cols/64)), built by the caller once per weight set; total_tiles = the sum over all n. Every
+// matrix must satisfy vj_transpose_bf16's constraints (checked by the caller when it builds desc).
+extern "C" int vj_transpose_bf16_batch(int n, const long* desc, long total_tiles, void* stream) {
+  if (n == 0 || total_tiles == 0) return VJ_OK;
+  VJ_CHECK_ARG(n > 0 && desc && total_tiles > 0, "vj_transpose_bf16_batch: bad arguments");
+  const long blocks = (total_tiles + 3) / 4;
+  const dim3 grid((unsigned)(blocks < 16384 ? blocks : 16384));
+  hipLaunchKernelGGL(k_transpose_bf16_batch, grid, dim3(256), 0, (hipStream_t)stream, desc, n, total_tiles);
+  VJ_LAUNCH_CHECK("vj_transpose_bf16_batch");
   return VJ_OK;
 }
 

@@ -10,6 +10,8 @@ operand is bf16 with f32 accumulation. Parameter gradients are accumulated (+=) 
 autograd only carries activation gradients between layers.
 """
 
+import weakref
+
 import torch
 
 from . import ops
@@ -39,7 +41,9 @@ SHADOW_EPOCH = [0]
 
 def weight_bf16_t(p):
     """W^T [in, out] bf16 contiguous: the K-major B operand of the data-gradient GEMM dX = dY W
-    (ops.linear_dgrad). Transposed by a HIP kernel once per weight update and cached."""
+    (ops.linear_dgrad). Transposed by a HIP kernel once per weight update and cached; the copies of
+    arena-owned weights are registered so refresh_weight_transposes() redoes them all in one launch
+    right after the update."""
     src = weight_bf16(p)
     arena_owned = getattr(p, "_vj_bf16", None) is not None
     key = (src.data_ptr(), SHADOW_EPOCH[0] if arena_owned else p._version)
@@ -48,7 +52,32 @@ def weight_bf16_t(p):
         out = c[1] if c is not None and c[1].shape == (src.shape[1], src.shape[0]) else None
         c = (key, ops.transpose_bf16(src.reshape(src.shape[0], -1), out=out))
         p._vj_bf16_t = c
+        if arena_owned:
+            _WT_REG[id(p)] = p
     return c[1]
+
+
+_WT_REG = weakref.WeakValueDictionary()  # id -> arena-owned parameter with a cached W^T copy
+_WT_BATCH = [None]  # (the batch's (src, dst) pointer key, device descriptor table, tiles)
+
+
+def refresh_weight_transposes():
+    """Re-transpose every registered W^T copy whose bf16 shadow changed (after AdamW / a weight
+    sync) with one vj_transpose_bf16_batch launch instead of one launch per weight in the backward."""
+    stale = [p for p in _WT_REG.values() if p._vj_bf16_t[0][1] != SHADOW_EPOCH[0]]
+    if not stale:
+        return
+    pairs = []
+    for p in stale:
+        src = weight_bf16(p)
+        pairs.append((src.reshape(src.shape[0], -1), p._vj_bf16_t[1]))
+    key = tuple((s.data_ptr(), d.data_ptr()) for s, d in pairs)
+    if _WT_BATCH[0] is None or _WT_BATCH[0][0] != key:
+        desc, tiles = ops.transpose_batch_desc(pairs)
+        _WT_BATCH[0] = (key, desc, tiles)
+    ops.transpose_bf16_batch(_WT_BATCH[0][1], len(pairs), _WT_BATCH[0][2])
+    for p, (s, _) in zip(stale, pairs):
+        p._vj_bf16_t = ((s.data_ptr(), SHADOW_EPOCH[0]), p._vj_bf16_t[1])
 
 
 def weight_fp8(p):

@@ -192,6 +192,29 @@ def transpose_bf16(x, out=None):
     return out
 
 
+def transpose_batch_desc(pairs):
+    """Device descriptor table of vj_transpose_bf16_batch for [(src [R, C], dst [C, R]), ...]:
+    int64 [n][8] = {src, dst, R, C, ld_src, ld_dst, first 64x64 tile, tiles across}. Returns (table,
+    total tiles). Built once per weight set (the pointers stay fixed)."""
+    rows, tiles = [], 0
+    for src, dst in pairs:
+        _dev(src, dst)
+        R, C = src.shape
+        assert src.dtype == BF16 and dst.dtype == BF16 and dst.shape == (C, R), (tuple(src.shape), tuple(dst.shape))
+        lds, ldd = _rowmajor(src, "src"), _rowmajor(dst, "dst")
+        if R % 8 or C % 8 or lds % 8 or ldd % 8 or (src.data_ptr() | dst.data_ptr()) & 15:
+            raise ValueError("transpose_batch_desc: rows, cols, strides must be multiples of 8, pointers 16-B aligned")
+        tx, ty = -(-C // 64), -(-R // 64)
+        rows.append([src.data_ptr(), dst.data_ptr(), R, C, lds, ldd, tiles, tx])
+        tiles += tx * ty
+    return torch.tensor(rows, dtype=torch.int64).to(pairs[0][0].device), tiles
+
+
+def transpose_bf16_batch(desc, n, tiles):
+    """One launch of n transposes described by transpose_batch_desc's table."""
+    _call("vj_transpose_bf16_batch", n, _p(desc), tiles, _stream())
+
+
 def _pad_cols(t):
     """[R, C] -> [R, C rounded up to 8], zero columns appended (GEMM operand rows are 16-B chunks)."""
     out = torch.zeros(t.shape[0], (t.shape[1] + 7) // 8 * 8, dtype=t.dtype, device=t.device)

@@ -29,6 +29,7 @@ from . import predictor as vit_pred
 from . import vision_transformer as video_vit
 from .arena import FlatArena, FusedAdamW, fused_ema, readiness_order, wd_split
 from .distributed import GradReducer, init_distributed
+from .functions import refresh_weight_transposes
 from .masks import MaskCollator, materialize
 from .schedulers import CosineWDSchedule, WarmupCosineSchedule
 from .wrappers import MultiSeqWrapper, PredictorMultiSeqWrapper
@@ -230,6 +231,7 @@ class JEPATrainer:
         self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused)
         self.opt.zero_grad()
         fused_ema(self.tgt_arenas, self.enc_arenas, momentum)
+        refresh_weight_transposes()  # the next backward's W^T operands, one launch
 
     def sync_bf16(self):
         for a in self.opt.arenas + self.tgt_arenas:

@@ -36,6 +36,7 @@ from .wrappers import MultiSeqWrapper, PredictorMultiSeqWrapper
 
 logger = logging.getLogger(__name__)
 _GLOBAL_SEED = 0
+_WT_BATCH = os.environ.get("VJ_WT_BATCH", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -231,7 +232,8 @@ class JEPATrainer:
         self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused)
         self.opt.zero_grad()
         fused_ema(self.tgt_arenas, self.enc_arenas, momentum)
-        refresh_weight_transposes()  # the next backward's W^T operands, one launch
+        if _WT_BATCH:  # the next backward's W^T operands, one launch (VJ_WT_BATCH=0: lazily, one per weight)
+            refresh_weight_transposes()
 
     def sync_bf16(self):
         for a in self.opt.arenas + self.tgt_arenas:

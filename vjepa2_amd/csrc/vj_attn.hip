@@ -40,6 +40,16 @@
 #endif
 
 // forward workgroups per CU the register budget is sized for (head dims <= 64)
+// forward, head dim 64: K / V^T fragments in rings (fewer live registers) at 4 workgroups per CU
+#ifndef VJ_ATTN_FWD_RING
+#define VJ_ATTN_FWD_RING 0
+#endif
+#ifndef VJ_ATTN_FWD_RING_V  // PV k-step after whose MFMAs the last two k-steps' V^T are read
+#define VJ_ATTN_FWD_RING_V 1
+#endif
+#ifndef VJ_ATTN_FWD_RING_OCC
+#define VJ_ATTN_FWD_RING_OCC 4
+#endif
 #ifndef VJ_ATTN_FWD_OCC
 #define VJ_ATTN_FWD_OCC 3
 #endif
@@ -211,8 +221,17 @@ __device__ __forceinline__ void stage_rows(__amdgpu_buffer_rsrc_t rs, long ld, i
     const int r = off / RB;
     const int phys = (off - r * RB) >> 4;
     const int c = phys ^ swz<HDP>(r);
-    const bool ok = (row0 + r) < nvalid && c < HD / 8;
-    const uint32_t voff = ok ? (uint32_t)(((long)(row0 + r) * ld + c * 8) * 2) : VJ_OOB;
+    uint32_t voff;
+    if constexpr (HD == HDP) {
+      // rows past the sequence end are out of the descriptor's range (every caller's descriptor
+      // spans exactly nvalid rows) and zero-fill without a per-lane test: one lane-constant register
+      // per piece (r * ld + c * 8) stays live across the sweep instead of offsets and masks
+      (void)nvalid;
+      voff = (uint32_t)(((long)(row0 + r) * ld + c * 8) * 2);
+    } else {
+      const bool ok = (row0 + r) < nvalid && c < HD / 8;
+      voff = ok ? (uint32_t)(((long)(row0 + r) * ld + c * 8) * 2) : VJ_OOB;
+    }
     dma16(rs, lds + p * 1024, voff);
   }
   (void)nwaves;
@@ -239,6 +258,37 @@ __device__ __forceinline__ bf16x8 tr_frag(const LDS_AS char* lds, int kb, int cb
   const s16x4 lo = ds_read_tr16_async(lds + lds_off<HDP>(r0, col >> 3) + within);
   const s16x4 hi = ds_read_tr16_async(lds + lds_off<HDP>(r1, col >> 3) + within);
   s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// tr_frag with the lane's addressing split off: for rows kb that are multiples of 16 the swizzle of
+// row kb + x equals that of row x (it reads row bits 1-3 only), so the byte offset of a fragment is
+// a per-lane part (tr_lane_off: column block d, half lo / hi) plus kb * row bytes, folded with the
+// image's own LDS position into the instruction's immediate. A sweep then holds 2 * HDP / 32
+// address registers instead of one per (k-step, column block, half).
+template <int HDP>
+__device__ __forceinline__ uint32_t tr_lane_off(int d, int half, int lane) {
+  const int h = lane >> 5;
+  const int q = (lane >> 2) & 3;
+  const int col = d * 32 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const int r = 4 * h + q + 8 * half;
+  return (uint32_t)(lds_off<HDP>(r, col >> 3) + (col & 7) * 2);
+}
+template <int IMM>
+__device__ __forceinline__ s16x4 ds_read_tr16_imm(uint32_t addr) {
+  static_assert(IMM >= 0 && IMM < 65536, "ds offset field");
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(IMM) : "memory");
+  return r;
+}
+// fragment (rows KB.., column block d) of the image at LDS byte IMG; lo / hi = tr_lane_off(d, 0 / 1)
+// + the LDS base address
+template <int HDP, int IMG, int KB>
+__device__ __forceinline__ bf16x8 tr_frag_at(uint32_t lo, uint32_t hi) {
+  static_assert(KB % 16 == 0, "row block must keep the swizzle phase");
+  const s16x4 a = ds_read_tr16_imm<IMG + KB * HDP * 2>(lo);
+  const s16x4 b = ds_read_tr16_imm<IMG + KB * HDP * 2>(hi);
+  s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8, v);
 }
 
@@ -312,8 +362,10 @@ constexpr float LOG2E = 1.4426950408889634f;
 // ------------------------------------------------------------------------------------------------
 // Forward: block = 4 waves x 32 queries, KV tiles of 64 keys double-buffered in LDS.
 template <int HD>
-__global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_fwd(AttnArgs a) {
+__global__ __launch_bounds__(256, (HD == 64 && VJ_ATTN_FWD_RING ? VJ_ATTN_FWD_RING_OCC : HD <= 64 ? VJ_ATTN_FWD_OCC : 2))
+void k_attn_fwd(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
+  constexpr bool RING = VJ_ATTN_FWD_RING && HD == 64;
   constexpr int KT = 64;
   constexpr int TB = KT * HDP * 2;  // bytes per K or V tile
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
@@ -360,6 +412,13 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_
   const float c = a.scale * LOG2E;
   const float tau = TAU / c;
 
+  // per-lane V^T read addresses (tr_frag_at): LDS base + lane part, d = column block
+  uint32_t vlo[HDP / 32], vhi[HDP / 32];
+#pragma unroll
+  for (int d = 0; d < HDP / 32; ++d) {
+    vlo[d] = (uint32_t)(uintptr_t)smem + tr_lane_off<HDP>(d, 0, lane);
+    vhi[d] = (uint32_t)(uintptr_t)smem + tr_lane_off<HDP>(d, 1, lane);
+  }
   const int nkt = (kend + KT - 1) / KT;
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
   stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
@@ -375,28 +434,56 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_
       stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
       stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
     }
-    // all K fragments first (one LDS wait), then two independent S^T chains interleaved
-    bf16x8 kf[2][HDP / 16];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int s = 0; s < HDP / 16; ++s) kf[kk][s] = row_frag<HDP>(Ks, kk * 32, s, lane);
     f32x16 st[2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
+    constexpr int VIMG = cur * 2 * TB + TB;
+    bf16x8 vf[4][HDP / 32];
+    if constexpr (RING) {
+      // K fragments in a ring of two k-steps (step s + 1 read under step s's two MFMAs) and only
+      // the first two k-steps of V^T read before the softmax (the other two under the PV MFMAs):
+      // the live registers fit four workgroups per CU
+      bf16x8 kr[2][2];
 #pragma unroll
-    for (int s = 0; s < HDP / 16; ++s)
+      for (int kk = 0; kk < 2; ++kk) kr[0][kk] = row_frag<HDP>(Ks, kk * 32, 0, lane);
+#pragma unroll
+      for (int s = 0; s < HDP / 16; ++s) {
+        if (s + 1 < HDP / 16)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) kr[(s + 1) & 1][kk] = row_frag<HDP>(Ks, kk * 32, s + 1, lane);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kr[s & 1][kk], qf[s], st[kk], 0, 0, 0);
+      }
+#pragma unroll
+      for (int d = 0; d < HDP / 32; ++d) {
+        vf[0][d] = tr_frag_at<HDP, VIMG, 0>(vlo[d], vhi[d]);
+        vf[1][d] = tr_frag_at<HDP, VIMG, 16>(vlo[d], vhi[d]);
+      }
+    } else {
+      // all K fragments first (one LDS wait), then two independent S^T chains interleaved
+      bf16x8 kf[2][HDP / 16];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][s], qf[s], st[kk], 0, 0, 0);
-    // V^T fragments: issued before the softmax so their LDS latency hides under it
-    bf16x8 vf[4][HDP / 32];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+        for (int s = 0; s < HDP / 16; ++s) kf[kk][s] = row_frag<HDP>(Ks, kk * 32, s, lane);
 #pragma unroll
-      for (int d = 0; d < HDP / 32; ++d) vf[ks][d] = tr_frag<HDP>(Vs, ks * 16, d * 32, lane);
+      for (int s = 0; s < HDP / 16; ++s)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][s], qf[s], st[kk], 0, 0, 0);
+      // V^T fragments: issued before the softmax so their LDS latency hides under it (per-lane base
+      // registers + immediates: the buffer and the k-step are compile-time)
+#pragma unroll
+      for (int d = 0; d < HDP / 32; ++d) {
+        vf[0][d] = tr_frag_at<HDP, VIMG, 0>(vlo[d], vhi[d]);
+        vf[1][d] = tr_frag_at<HDP, VIMG, 16>(vlo[d], vhi[d]);
+        vf[2][d] = tr_frag_at<HDP, VIMG, 32>(vlo[d], vhi[d]);
+        vf[3][d] = tr_frag_at<HDP, VIMG, 48>(vlo[d], vhi[d]);
+      }
+    }
     const int kb = kt * KT;
     if (kb + KT > kmask0) {  // ragged last tile (or frame-causal boundary tiles): keys past the limit get -inf
       asm volatile("");  // keeps the compiler from if-converting this into every tile
@@ -438,13 +525,38 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_FWD_OCC : 2)) void k_attn_
     lsum += ls0 + ls1;
     // O^T += V^T P^T over 4 key-steps of 16
     lds_wait();
+    if constexpr (RING) {
+      tie(vf[0]);
+      tie(vf[1]);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) tie(vf[ks]);
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks == 2) {  // the last two k-steps' V^T, read under the first two's MFMAs
+          lds_wait();
+          tie(vf[2]);
+          tie(vf[3]);
+        }
+        const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
+        for (int d = 0; d < HDP / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
+        if (ks == VJ_ATTN_FWD_RING_V) {
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int d = 0; d < HDP / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
+          for (int d = 0; d < HDP / 32; ++d) {
+            vf[2][d] = tr_frag_at<HDP, VIMG, 32>(vlo[d], vhi[d]);
+            vf[3][d] = tr_frag_at<HDP, VIMG, 48>(vlo[d], vhi[d]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) tie(vf[ks]);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
+#pragma unroll
+        for (int d = 0; d < HDP / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
+      }
     }
     __syncthreads();
   };
@@ -610,6 +722,13 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
     }
   };
 
+  // per-lane transposed-read addresses (tr_frag_at) of the Q / dO images
+  uint32_t tlo[HDP / 32], thi[HDP / 32];
+#pragma unroll
+  for (int d = 0; d < HDP / 32; ++d) {
+    tlo[d] = (uint32_t)(uintptr_t)smem + tr_lane_off<HDP>(d, 0, lane);
+    thi[d] = (uint32_t)(uintptr_t)smem + tr_lane_off<HDP>(d, 1, lane);
+  }
   const int nqt = (len + QT - 1) / QT;
   // frame-causal: key k is seen by queries from its frame block's start on; the sweep starts at the
   // block's first key's frame start, and query tiles before its last key's frame start take the mask
@@ -714,8 +833,10 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
       for (int d = 0; d < HDP / 32; ++d) {
-        dtf[s2][d] = tr_frag<HDP>(Ds, s2 * 16, d * 32, lane);
-        qtf[s2][d] = tr_frag<HDP>(Qs, s2 * 16, d * 32, lane);
+        dtf[s2][d] = s2 ? tr_frag_at<HDP, cur * STAGE + TB, 16>(tlo[d], thi[d])
+                        : tr_frag_at<HDP, cur * STAGE + TB, 0>(tlo[d], thi[d]);
+        qtf[s2][d] = s2 ? tr_frag_at<HDP, cur * STAGE, 16>(tlo[d], thi[d])
+                        : tr_frag_at<HDP, cur * STAGE, 0>(tlo[d], thi[d]);
       }
     if (qt * QT < qmask_end) {  // frame-causal: queries of earlier frames than the key see nothing
       asm volatile("");
@@ -808,11 +929,14 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
 // dQ: block = 4 waves x (32 QW) queries; sweep key tiles of 64 (K, V staged in LDS). Each wave owns
 // QW 32-query tiles (tile qw of wave w: queries qw*128 + w*32 + 0..31 of the block), so every K / V
 // fragment read from LDS feeds QW independent MFMA chains.
+#ifndef VJ_ATTN_DQ64_OCC  // head dim 64: 3 fits 168 VGPRs (2 dwords spilled)
+#define VJ_ATTN_DQ64_OCC 1
+#endif
 #ifndef VJ_ATTN_DQ_OCC
 #define VJ_ATTN_DQ_OCC 1
 #endif
 template <int HD, int QW>
-__global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_bwd_dq(AttnArgs a) {
+__global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_bwd_dq(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr int KT = 64;
   constexpr int TB = KT * HDP * 2;
@@ -880,6 +1004,13 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_b
   const int kend = fc_klim(a.fblk, min(q_first + 128 * QW - 1, len - 1), len);
   const int kmask0 = fc_klim(a.fblk, q_first, len);
 
+  // per-lane transposed-read addresses (tr_frag_at) of the K images
+  uint32_t klo[HDP / 32], khi[HDP / 32];
+#pragma unroll
+  for (int d = 0; d < HDP / 32; ++d) {
+    klo[d] = (uint32_t)(uintptr_t)smem + tr_lane_off<HDP>(d, 0, lane);
+    khi[d] = (uint32_t)(uintptr_t)smem + tr_lane_off<HDP>(d, 1, lane);
+  }
   const int nkt = (kend + KT - 1) / KT;
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
   stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
@@ -909,7 +1040,11 @@ __global__ __launch_bounds__(256, (HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_b
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-        for (int d = 0; d < HDP / 32; ++d) ktf[s2][d] = tr_frag<HDP>(Ks, kk * 32 + s2 * 16, d * 32, lane);
+        for (int d = 0; d < HDP / 32; ++d)
+          ktf[s2][d] = (kk * 2 + s2 == 0)   ? tr_frag_at<HDP, cur * 2 * TB, 0>(klo[d], khi[d])
+                       : (kk * 2 + s2 == 1) ? tr_frag_at<HDP, cur * 2 * TB, 16>(klo[d], khi[d])
+                       : (kk * 2 + s2 == 2) ? tr_frag_at<HDP, cur * 2 * TB, 32>(klo[d], khi[d])
+                                            : tr_frag_at<HDP, cur * 2 * TB, 48>(klo[d], khi[d]);
       f32x16 st[QW], dpt[QW];
 #pragma unroll
       for (int qw = 0; qw < QW; ++qw)

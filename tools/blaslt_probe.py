@@ -16,6 +16,9 @@ SHAPES = [  # (name, M, N, K, a_transposed, b_transposed): C[M,N] = A[M,K] B[K,N
     ("wgrad qkv dY^T X", 3072, 1024, 11712, True, False),
     ("pred wgrad fc1", 1536, 384, 71232, True, False),
     ("pred fc1 X W^T", 71232, 1536, 384, False, True),
+    ("wgrad fc2 dY^T X", 1024, 4096, 11712, True, False),
+    ("wgrad proj dY^T X", 1024, 1024, 11712, True, False),
+    ("pred wgrad qkv", 1152, 384, 71232, True, False),
 ]
 
 

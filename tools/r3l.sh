@@ -9,3 +9,5 @@ for r in 1 2; do
   done
 done
 bash tools/vitg_final.sh r03vitg
+timeout -k 10 200 python -u tools/blaslt_probe.py > gpurun_out/r3n/blaslt.log 2>&1 || { echo "blaslt probe failed"; tail -5 gpurun_out/r3n/blaslt.log; exit 6; }
+cat gpurun_out/r3n/blaslt.log

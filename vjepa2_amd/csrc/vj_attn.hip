@@ -929,8 +929,8 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
 // dQ: block = 4 waves x (32 QW) queries; sweep key tiles of 64 (K, V staged in LDS). Each wave owns
 // QW 32-query tiles (tile qw of wave w: queries qw*128 + w*32 + 0..31 of the block), so every K / V
 // fragment read from LDS feeds QW independent MFMA chains.
-#ifndef VJ_ATTN_DQ64_OCC  // head dim 64: 3 fits 168 VGPRs (2 dwords spilled)
-#define VJ_ATTN_DQ64_OCC 1
+#ifndef VJ_ATTN_DQ64_OCC  // head dim 64: 3 workgroups per CU at 168 VGPRs (one dword reloaded per key tile): bwd -2..-3 % (bench_kernels)
+#define VJ_ATTN_DQ64_OCC 3
 #endif
 #ifndef VJ_ATTN_DQ_OCC
 #define VJ_ATTN_DQ_OCC 1

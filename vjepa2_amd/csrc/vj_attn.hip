@@ -50,6 +50,9 @@
 #ifndef VJ_ATTN_FWD_RING_OCC
 #define VJ_ATTN_FWD_RING_OCC 4
 #endif
+#ifndef VJ_ATTN_FWD32_OCC  // head dim 32 (predictor): 102 VGPRs hold 4 workgroups per CU
+#define VJ_ATTN_FWD32_OCC 3
+#endif
 #ifndef VJ_ATTN_FWD_OCC
 #define VJ_ATTN_FWD_OCC 3
 #endif
@@ -362,7 +365,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 // ------------------------------------------------------------------------------------------------
 // Forward: block = 4 waves x 32 queries, KV tiles of 64 keys double-buffered in LDS.
 template <int HD>
-__global__ __launch_bounds__(256, (HD == 64 && VJ_ATTN_FWD_RING ? VJ_ATTN_FWD_RING_OCC : HD <= 64 ? VJ_ATTN_FWD_OCC : 2))
+__global__ __launch_bounds__(256, (HD == 64 && VJ_ATTN_FWD_RING ? VJ_ATTN_FWD_RING_OCC : HD == 32 ? VJ_ATTN_FWD32_OCC : HD <= 64 ? VJ_ATTN_FWD_OCC : 2))
 void k_attn_fwd(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr bool RING = VJ_ATTN_FWD_RING && HD == 64;

@@ -47,6 +47,8 @@ def build(verbose=True, force=False, variant=None, defines=()):
     objdir = os.path.join(HERE, "build", variant) if variant else os.path.join(HERE, "build")
     lib = os.path.join(HERE, f"libvjepa_hip_{variant}.so") if variant else LIB
     flags = CFLAGS + [f"-D{d}" for d in defines]
+    if variant:  # experiments: extra compiler flags for every source (e.g. VJ_EXTRA_FLAGS=-fno-slp-vectorize)
+        flags += os.environ.get("VJ_EXTRA_FLAGS", "").split()
     os.makedirs(objdir, exist_ok=True)
     jobs = []
     csrc = os.environ.get("VJ_CSRC", CSRC) if variant else CSRC  # variant may build another source tree

@@ -501,7 +501,7 @@ void k_attn_fwd(AttnArgs a) {
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, st[0][r]);
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[1][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_xor32(mx);
     if (__builtin_amdgcn_ballot_w64(mx > m_use + tau)) {
       asm volatile("");  // a real (rare) branch, not if-converted into every tile
       const float m_new = fmaxf(m_use, mx);
@@ -567,7 +567,7 @@ void k_attn_fwd(AttnArgs a) {
     tile_iter(kt0, std::integral_constant<int, 0>{});
     if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
   }
-  const float l_tot = lsum + __shfl_xor(lsum, 32, 64);
+  const float l_tot = sum_xor32(lsum);
   const float inv = 1.f / l_tot;
   if (qok) {
     bf16_t* orow = a.o + (long)(seq0 + qloc) * a.ldo + h * HD;
@@ -976,7 +976,7 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
 #pragma unroll
         for (int j = 0; j < 8; ++j) sd = fmaf((float)gf[qw][s][j], (float)ov[j], sd);
       }
-      sd += __shfl_xor(sd, 32, 64);
+      sd = sum_xor32(sd);
       dl[qw] = qok[qw] ? -sd : 0.f;
       if (qok[qw] && hl == 0) a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc[qw]] = -sd;
     } else {

@@ -56,16 +56,56 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }
 
-// ----- wave reductions (64 lanes) -----
+// ----- cross-lane exchanges on the VALU (DPP / gfx950 permlane swaps) -----
+// __shfl_xor compiles to ds_bpermute_b32, an LDS-unit round trip (~100+ cycles) per step; these stay
+// in the vector ALU. Each pairs lane l with a partner and both lanes compute the same commutative
+// op, so every lane ends with the bitwise-identical result.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+constexpr int DPP_XOR1 = 0xB1;        // quad_perm [1, 0, 3, 2]: lane l <-> l ^ 1
+constexpr int DPP_XOR2 = 0x4E;        // quad_perm [2, 3, 0, 1]: lane l <-> l ^ 2
+constexpr int DPP_HALF_MIRROR = 0x141;  // within 8 lanes: i <-> 7 - i
+constexpr int DPP_MIRROR = 0x140;       // within 16 lanes: i <-> 15 - i
+// (own, partner) pairs: lane l <-> l ^ 16 / l ^ 32 (v_permlane16_swap / v_permlane32_swap)
+__device__ __forceinline__ float sum_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float max_xor16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// ----- wave reductions (64 lanes; every lane gets the total) -----
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp<DPP_XOR1>(v);         // pairs
+  v += dpp<DPP_XOR2>(v);         // quads
+  v += dpp<DPP_HALF_MIRROR>(v);  // 8 lanes: quad sums of both halves
+  v += dpp<DPP_MIRROR>(v);       // 16 lanes
+  v = sum_xor16(v);              // 32
+  return sum_xor32(v);           // 64
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp<DPP_XOR1>(v));
+  v = fmaxf(v, dpp<DPP_XOR2>(v));
+  v = fmaxf(v, dpp<DPP_HALF_MIRROR>(v));
+  v = fmaxf(v, dpp<DPP_MIRROR>(v));
+  v = max_xor16(v);
+  return max_xor32(v);
 }
 
 // ----- buffer resource (SRD) for LDS-DMA loads with hardware range check -----

@@ -475,7 +475,7 @@ __global__ __launch_bounds__(512, 2) void k_gemm_pp(G256 g) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) snd[k] = odd ? pk[k >> 1][k & 1] : pk[2 + (k >> 1)][k & 1];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) rcv[k] = (uint32_t)__shfl_xor((int)snd[k], 1, 64);
+      for (int k = 0; k < 4; ++k) rcv[k] = dpp_u<DPP_XOR1>(snd[k]);  // lane pair exchange on the VALU
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int r = odd ? 2 + h : h;

@@ -188,6 +188,12 @@ int vj_check_finite(long n, const float* g, int* found_inf, void* stream);
 int vj_adamw(long n, float* p, const float* g, float* m, float* v, void* p_bf16, float lr, float beta1, float beta2,
              float eps, float weight_decay, int step, float grad_scale, const int* found_inf, void* stream);
 int vj_ema(long n, float* target, const float* online, float momentum, void* target_bf16, void* stream);
+/* vj_adamw + vj_ema in one pass (train.py:443-465): the parameters are updated, then
+ * target = target * momentum + (1 - momentum) * p from the new values (on a step skipped by found_inf,
+ * from the unchanged ones) with its bf16 shadow; target / target_bf16 NULL = plain vj_adamw. */
+int vj_adamw_ema(long n, float* p, const float* g, float* m, float* v, void* p_bf16, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, int step, float grad_scale, const int* found_inf,
+                 float* target, void* target_bf16, float momentum, void* stream);
 int vj_cast_bf16(long n, const float* in, void* out, void* stream);
 /* dst[c][r] = src[r][c] (bf16; rows, cols, strides multiples of 8): the K-major copy W^T that the
  * data-gradient GEMM dX = dY W (nn.Linear backward) reads as its B operand. */

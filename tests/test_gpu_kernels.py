@@ -631,6 +631,36 @@ def test_adamw_ema_match_oracle():
     assert torch.equal(tbf, td.bfloat16())
 
 
+@pytest.mark.parametrize("skip", [False, True])
+def test_adamw_ema_fused_equals_separate(skip):
+    """vj_adamw_ema (the EMA fused into the encoder arena's AdamW pass) == vj_adamw then vj_ema,
+    bitwise, including a step skipped by found_inf (parameters unchanged, the EMA still applied)."""
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(16)
+    n = 8192
+    base = [torch.randn(n, generator=g), torch.randn(n, generator=g), 0.1 * torch.randn(n, generator=g),
+            torch.rand(n, generator=g), torch.randn(n, generator=g)]
+    flag = torch.tensor([1 if skip else 0], dtype=torch.int32, device=DEV)
+    outs = []
+    for fused in (True, False):
+        p, gr, m, v, t = (x.clone().to(DEV) for x in base)
+        pbf = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        tbf = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+        if fused:
+            ops.adamw_ema(p, gr, m, v, pbf, 5e-4, 0.9, 0.999, 1e-8, 0.04, 3, t, tbf, 0.99925, grad_scale=0.5,
+                          found_inf=flag)
+        else:
+            ops.adamw(p, gr, m, v, pbf, 5e-4, 0.9, 0.999, 1e-8, 0.04, 3, grad_scale=0.5, found_inf=flag)
+            ops.ema(t, p, 0.99925, tbf)
+        torch.cuda.synchronize()
+        outs.append((p, m, v, t, tbf))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    if skip:
+        assert torch.equal(outs[0][0].cpu(), base[0])
+
+
 @pytest.mark.parametrize("K", [64, 192, 256, 1024])
 @pytest.mark.parametrize("pxcd", [None, "1", "3"])
 def test_gemm_pingpong_matches_one_tile_kernel(K, pxcd, monkeypatch):

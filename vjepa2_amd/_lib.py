@@ -61,6 +61,7 @@ SIGNATURES = {
     "vj_check_finite": [_L, _P, _P, _P],
     "vj_adamw": [_L, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, _P, _P],
     "vj_ema": [_L, _P, _P, _F, _P, _P],
+    "vj_adamw_ema": [_L, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, _P, _P, _P, _F, _P],
     "vj_cast_bf16": [_L, _P, _P, _P],
     "vj_transpose_bf16": [_I, _I, _P, _L, _P, _L, _P],
     "vj_transpose_bf16_batch": [_I, _P, _L, _P],

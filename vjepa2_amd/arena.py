@@ -182,12 +182,17 @@ class FusedAdamW:
                 self.pstep[i][idx] -= 1
         self._pending = None
 
-    def step(self, grad_scale=1.0, found_inf=None, exclude=()):
+    def step(self, grad_scale=1.0, found_inf=None, exclude=(), ema=None):
+        """One AdamW step over every arena. ema = (targets, momentum), targets[i] the target arena of
+        arena i (same layout) or None: the EMA of train.py:456-465 is fused into the AdamW pass of that
+        arena (the online parameters are read once); an arena with excluded parameters gets the plain
+        EMA after its AdamW instead."""
         self._resolve()
         for a in self.arenas:
             a.finalize_grads()
         ex = {id(p) for p in exclude}
         advanced = []
+        late_ema = []
         for i, (g, a) in enumerate(zip(self.param_groups, self.arenas)):
             act = np.array([id(p) not in ex for p in a.params], dtype=bool)
             st = self.pstep[i]
@@ -195,8 +200,12 @@ class FusedAdamW:
             advanced.append((i, np.nonzero(act)[0]))
             b1, b2 = g["betas"]
             wd = 0.0 if g.get("WD_exclude", False) else g["weight_decay"]
+            tgt = ema[0][i] if ema is not None else None
+            fuse = tgt is not None and bool(act.all()) and tgt.numel == a.numel
+            if tgt is not None and not fuse:
+                late_ema.append((tgt, a))
             j, n = 0, len(a.params)
-            while j < n:  # maximal runs of active params with equal step count
+            while j < n:  # maximal runs of active params with equal step count (they tile the arena when all are active)
                 if not act[j]:
                     j += 1
                     continue
@@ -204,9 +213,16 @@ class FusedAdamW:
                 while k < n and act[k] and st[k] == st[j]:
                     k += 1
                 lo, hi = a.span(j, k)
-                ops.adamw(a.data[lo:hi], a.grad[lo:hi], a.exp_avg[lo:hi], a.exp_avg_sq[lo:hi], a.bf16[lo:hi], g["lr"],
-                          b1, b2, g["eps"], wd, int(st[j]), grad_scale=grad_scale, found_inf=found_inf)
+                if fuse:
+                    ops.adamw_ema(a.data[lo:hi], a.grad[lo:hi], a.exp_avg[lo:hi], a.exp_avg_sq[lo:hi], a.bf16[lo:hi],
+                                  g["lr"], b1, b2, g["eps"], wd, int(st[j]), tgt.data[lo:hi], tgt.bf16[lo:hi], ema[1],
+                                  grad_scale=grad_scale, found_inf=found_inf)
+                else:
+                    ops.adamw(a.data[lo:hi], a.grad[lo:hi], a.exp_avg[lo:hi], a.exp_avg_sq[lo:hi], a.bf16[lo:hi],
+                              g["lr"], b1, b2, g["eps"], wd, int(st[j]), grad_scale=grad_scale, found_inf=found_inf)
                 j = k
+        for t, a in late_ema:
+            ops.ema(t.data, a.data, ema[1], t.bf16)
         SHADOW_EPOCH[0] += 1  # the bf16 shadows changed: cached W^T copies are stale
         if found_inf is not None:
             flag = torch.empty(1, dtype=torch.int32, pin_memory=True)

@@ -21,6 +21,14 @@
 #include <type_traits>
 #include "vj_gemm_tile.h"
 
+// 8-wave main loop: the next K-tile's DMA pieces issued between the last phase's MFMAs instead of in
+// one burst after the barrier (1: B pieces halfway; 2: A pieces after the first quarter as well).
+// Measured (tools/bench_kernels.py, profiles/r03_gemm_spread_kernels.txt): 1 = -2..-7 % on the
+// ViT-L forward / data-gradient shapes.
+#ifndef VJ_GEMM_SPREAD
+#define VJ_GEMM_SPREAD 1
+#endif
+
 namespace {
 
 #if VJ_GEMM_STAMPS  // diagnostic build: s_memtime per tile (start, main loop done, epilogue done) of wave 0
@@ -224,6 +232,15 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     __builtin_amdgcn_s_setprio(0);
 #endif
   };
+  // m-tiles i0 .. i1 - 1 of one phase (SPREAD splits the last phase around the B DMA pieces)
+  auto mm_rows = [&](const bf16x8 (&X)[4], int mh, const bf16x8 (&Y)[NTN], int i0, int i1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i >= i0 && i < i1)
+#pragma unroll
+        for (int j = 0; j < NTN; ++j)
+          acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * 4 + i][j], 0, 0, 0);
+  };
   // MN-major operands are read with asm transposed reads (ds_read_tr16_async): each phase first
   // waits for the fragments it consumes (read in the previous phase), then issues the next reads.
   constexpr bool ASYNC = !AK || !BKM;
@@ -344,8 +361,18 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      // SPREAD (8-wave, bf16, main loop): only the A pieces of K-tile t + 2 go out here; the B pieces
+      // are issued between the two halves of the last phase's MFMAs, so the post-barrier DMA burst of
+      // both waves of a SIMD is half as long
+      constexpr bool SPREAD = VJ_GEMM_SPREAD && NWV == 8 && !F8 && BK == 64;
       if constexpr (!TAIL) {
-        load_k(ra, rb, cur, t + 2, sl, lane);
+        if constexpr (SPREAD) {
+          if (VJ_GEMM_SPREAD == 1 && (DMAW == 8 || wave < DMAW))
+            stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff, smem + sl * STAGE,
+                                                 wave, lane);
+        } else {
+          load_k(ra, rb, cur, t + 2, sl, lane);
+        }
       } else if (has_next) {
         // slot sl is free: the next tile's stage 0 (t == nk-2) or stage 1 (t == nk-1; stage 0 goes
         // to the other, unused slot when nk == 1); stage 1 waits for the epilogue unless EARLY1
@@ -383,7 +410,27 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         rdB(Ba, sl ^ 1, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      mm(Ab, 1, Bb);
+      if constexpr (SPREAD && !TAIL) {
+        if constexpr (VJ_GEMM_SPREAD == 2) {  // the A pieces after the first m-tile's MFMAs as well
+          mm_rows(Ab, 1, Bb, 0, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          if (DMAW == 8 || wave < DMAW)
+            stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff, smem + sl * STAGE,
+                                                 wave, lane);
+          __builtin_amdgcn_sched_barrier(0);
+          mm_rows(Ab, 1, Bb, 1, 2);
+        } else {
+          mm_rows(Ab, 1, Bb, 0, 2);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (DMAW == 8 || wave < DMAW)
+          stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
+                                                 smem + sl * STAGE + A_BYTES, wave, lane);
+        __builtin_amdgcn_sched_barrier(0);
+        mm_rows(Ab, 1, Bb, 2, 4);
+      } else {
+        mm(Ab, 1, Bb);
+      }
       __builtin_amdgcn_sched_barrier(0);
       }
     };

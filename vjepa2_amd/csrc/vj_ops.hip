@@ -909,29 +909,50 @@ struct AdamHP {
   float eps;
   float grad_scale;  // gradients are multiplied by this first (1/world for an unaveraged sum)
 };
+// EMA (optional, t != nullptr): the target encoder's update from the just-updated parameters, fused
+// so the online parameters are not read a second time (target <- target * mom + (1 - mom) * p, the
+// two roundings of k_ema); on a skipped step (found_inf) the EMA still runs, on the old parameters,
+// as train.py:446-465 does after a skipped scaler.step.
 __global__ void k_adamw(long n4, float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ m,
-                        float4* __restrict__ v, uint2* __restrict__ pbf, AdamHP hp, const int* __restrict__ found_inf) {
-  if (found_inf && *found_inf) return;  // GradScaler.step semantics: skip the update on inf/NaN
+                        float4* __restrict__ v, uint2* __restrict__ pbf, AdamHP hp, const int* __restrict__ found_inf,
+                        float4* __restrict__ t = nullptr, uint2* __restrict__ tbf = nullptr, float mom = 0.f,
+                        float one_m = 0.f) {
+  const bool skip = found_inf && *found_inf;  // GradScaler.step semantics: skip the update on inf/NaN
+  if (skip && !t) return;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    float pp[4], gg[4], mm[4], vv[4];
+    float pp[4];
     *(float4*)pp = p[i];
-    *(float4*)gg = g[i];
-    *(float4*)mm = m[i];
-    *(float4*)vv = v[i];
+    if (!skip) {
+      float gg[4], mm[4], vv[4];
+      *(float4*)gg = g[i];
+      *(float4*)mm = m[i];
+      *(float4*)vv = v[i];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float gr = gg[j] * hp.grad_scale;
-      pp[j] = pp[j] * hp.decay;
-      mm[j] = mm[j] + hp.one_m_b1 * (gr - mm[j]);
-      vv[j] = vv[j] * hp.beta2;
-      vv[j] = vv[j] + hp.one_m_b2 * gr * gr;
-      const float den = sqrtf(vv[j]) / hp.bc2_sqrt + hp.eps;
-      pp[j] = pp[j] + hp.neg_step * (mm[j] / den);
+      for (int j = 0; j < 4; ++j) {
+        const float gr = gg[j] * hp.grad_scale;
+        pp[j] = pp[j] * hp.decay;
+        mm[j] = mm[j] + hp.one_m_b1 * (gr - mm[j]);
+        vv[j] = vv[j] * hp.beta2;
+        vv[j] = vv[j] + hp.one_m_b2 * gr * gr;
+        const float den = sqrtf(vv[j]) / hp.bc2_sqrt + hp.eps;
+        pp[j] = pp[j] + hp.neg_step * (mm[j] / den);
+      }
+      p[i] = *(float4*)pp;
+      m[i] = *(float4*)mm;
+      v[i] = *(float4*)vv;
+      if (pbf) pbf[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
     }
-    p[i] = *(float4*)pp;
-    m[i] = *(float4*)mm;
-    v[i] = *(float4*)vv;
-    if (pbf) pbf[i] = make_uint2(pack_bf2(pp[0], pp[1]), pack_bf2(pp[2], pp[3]));
+    if (t) {
+      float a[4];
+      *(float4*)a = t[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = a[j] * mom;
+        a[j] = x + one_m * pp[j];
+      }
+      t[i] = *(float4*)a;
+      if (tbf) tbf[i] = make_uint2(pack_bf2(a[0], a[1]), pack_bf2(a[2], a[3]));
+    }
   }
 }
 
@@ -1290,12 +1311,35 @@ extern "C" int vj_check_finite(long n, const float* g, int* found_inf, void* str
   return VJ_OK;
 }
 
+static AdamHP adam_hp(float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale);
+extern "C" int vj_adamw_ema(long n, float* p, const float* g, float* m, float* v, void* p_bf16, float lr, float beta1,
+                            float beta2, float eps, float weight_decay, int step, float grad_scale, const int* found_inf,
+                            float* target, void* target_bf16, float momentum, void* stream);
+
 extern "C" int vj_adamw(long n, float* p, const float* g, float* m, float* v, void* p_bf16, float lr, float beta1,
                         float beta2, float eps, float weight_decay, int step, float grad_scale, const int* found_inf,
                         void* stream) {
+  return vj_adamw_ema(n, p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_scale, found_inf, nullptr,
+                      nullptr, 0.f, stream);
+}
+
+extern "C" int vj_adamw_ema(long n, float* p, const float* g, float* m, float* v, void* p_bf16, float lr, float beta1,
+                            float beta2, float eps, float weight_decay, int step, float grad_scale, const int* found_inf,
+                            float* target, void* target_bf16, float momentum, void* stream) {
   if (n == 0) return VJ_OK;
   VJ_CHECK_ARG(n % 4 == 0, "vj_adamw: n must be %%4");
   VJ_CHECK_ARG(step >= 1, "vj_adamw: step must be >= 1");
+  VJ_CHECK_ARG(target || !target_bf16, "vj_adamw_ema: target_bf16 without target");
+  const AdamHP hp = adam_hp(lr, beta1, beta2, eps, weight_decay, step, grad_scale);
+  const long n4 = n / 4;
+  hipLaunchKernelGGL(k_adamw, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4, (float4*)p,
+                     (const float4*)g, (float4*)m, (float4*)v, (uint2*)p_bf16, hp, found_inf, (float4*)target,
+                     (uint2*)target_bf16, momentum, (float)(1.0 - (double)momentum));
+  VJ_LAUNCH_CHECK("vj_adamw");
+  return VJ_OK;
+}
+
+static AdamHP adam_hp(float lr, float beta1, float beta2, float eps, float weight_decay, int step, float grad_scale) {
   AdamHP hp;
   const double bc1 = 1.0 - pow((double)beta1, step);
   const double bc2 = 1.0 - pow((double)beta2, step);
@@ -1308,11 +1352,7 @@ extern "C" int vj_adamw(long n, float* p, const float* g, float* m, float* v, vo
   hp.bc2_sqrt = (float)sqrt(bc2);
   hp.eps = eps;
   hp.grad_scale = grad_scale;
-  const long n4 = n / 4;
-  hipLaunchKernelGGL(k_adamw, dim3(grid_stride_blocks(n4)), dim3(256), 0, (hipStream_t)stream, n4, (float4*)p,
-                     (const float4*)g, (float4*)m, (float4*)v, (uint2*)p_bf16, hp, found_inf);
-  VJ_LAUNCH_CHECK("vj_adamw");
-  return VJ_OK;
+  return hp;
 }
 
 extern "C" int vj_ema(long n, float* target, const float* online, float momentum, void* target_bf16, void* stream) {

@@ -579,6 +579,16 @@ def adamw(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, grad_sc
          float(eps), float(weight_decay), int(step), float(grad_scale), _p(found_inf), _stream())
 
 
+def adamw_ema(p, g, m, v, p_bf16, lr, beta1, beta2, eps, weight_decay, step, target, target_bf16, momentum,
+              grad_scale=1.0, found_inf=None):
+    """adamw() followed by ema(target, p, momentum, target_bf16) in one pass over the arena slice."""
+    _dev(p, g, m, v, p_bf16, found_inf, target, target_bf16)
+    assert target.shape == p.shape and target.dtype == F32
+    _call("vj_adamw_ema", p.numel(), _p(p), _p(g), _p(m), _p(v), _p(p_bf16), float(lr), float(beta1), float(beta2),
+          float(eps), float(weight_decay), int(step), float(grad_scale), _p(found_inf), _p(target), _p(target_bf16),
+          float(momentum), _stream(), label="vj_adamw")
+
+
 def ema(target, online, momentum, target_bf16=None):
     _dev(target, online, target_bf16)
     _call("vj_ema", target.numel(), _p(target), _p(online), float(momentum), _p(target_bf16), _stream())

@@ -37,6 +37,7 @@ from .wrappers import MultiSeqWrapper, PredictorMultiSeqWrapper
 logger = logging.getLogger(__name__)
 _GLOBAL_SEED = 0
 _WT_BATCH = os.environ.get("VJ_WT_BATCH", "1") != "0"
+_FUSED_EMA = os.environ.get("VJ_FUSED_EMA", "1") != "0"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -229,9 +230,15 @@ class JEPATrainer:
         found = self.opt.check_finite() if self.mixed_precision else None
         used = {i % max(1, len(self.mask_tokens)) for i in range(getattr(self, "_groups", 1))}
         unused = [t for i, t in enumerate(self.mask_tokens) if i not in used]
-        self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused)
-        self.opt.zero_grad()
-        fused_ema(self.tgt_arenas, self.enc_arenas, momentum)
+        if _FUSED_EMA:  # the EMA inside the encoder arenas' AdamW pass (one read of the online weights)
+            tmap = {id(o): t for t, o in zip(self.tgt_arenas, self.enc_arenas)}
+            self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused,
+                          ema=([tmap.get(id(a)) for a in self.opt.arenas], momentum))
+            self.opt.zero_grad()
+        else:
+            self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused)
+            self.opt.zero_grad()
+            fused_ema(self.tgt_arenas, self.enc_arenas, momentum)
         if _WT_BATCH:  # the next backward's W^T operands, one launch (VJ_WT_BATCH=0: lazily, one per weight)
             refresh_weight_transposes()
 

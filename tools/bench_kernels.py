@@ -233,20 +233,21 @@ def main():
     libs = [load(pth) for pth in paths]
     cases = []
     only = os.environ.get("VJ_BENCH_ONLY", "")
+    kind = os.environ.get("VJ_BENCH_KIND", "")  # gemm | attn | ln: one family only
     for c in GEMMS:
-        if only and only not in c[0]:
+        if (only and only not in c[0]) or kind not in ("", "gemm"):
             continue
         cases.append((c[0], [gemm_case(lib, c, dev, stream) for lib in libs]))
     for name, hd, H, groups, bwd in ATTN:
-        if only and only not in name:
+        if (only and only not in name) or kind not in ("", "attn"):
             continue
         cases.append((name, [attn_case(lib, hd, H, groups, dev, stream, bwd) for lib in libs]))
     for name, M, D, xbf in LNF:
-        if only and only not in name:
+        if (only and only not in name) or kind not in ("", "ln"):
             continue
         cases.append((name, [ln_fwd_case(lib, M, D, xbf, dev, stream) for lib in libs]))
     for name, M, D, acc in LNB:
-        if only and only not in name:
+        if (only and only not in name) or kind not in ("", "ln"):
             continue
         cases.append((name, [ln_bwd_case(lib, M, D, acc, dev, stream) for lib in libs]))
     names = [os.path.basename(p).replace("libvjepa_hip", "lib")[:14] + ("@" + ",".join(f"{k[7:] if k.startswith('VJ_GEMM_') else k}={v}" for k, v in e.items()) if e else "") for p, e in cols]

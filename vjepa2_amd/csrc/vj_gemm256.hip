@@ -28,6 +28,12 @@
 #ifndef VJ_GEMM_SPREAD
 #define VJ_GEMM_SPREAD 1
 #endif
+#ifndef VJ_GEMM_SPREAD32
+#define VJ_GEMM_SPREAD32 0
+#endif
+#ifndef VJ_GEMM_SPLIT_AT
+#define VJ_GEMM_SPLIT_AT 2
+#endif
 
 namespace {
 
@@ -365,9 +371,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // are issued between the two halves of the last phase's MFMAs, so the post-barrier DMA burst of
       // both waves of a SIMD is half as long
       constexpr bool SPREAD = VJ_GEMM_SPREAD && NWV == 8 && !F8 && BK == 64;
+      // the same for the two-workgroup kernel's 32-deep K-tiles (one phase after the barrier)
+      constexpr bool SPREAD32 = VJ_GEMM_SPREAD32 && NWV == 4 && BK == 32;
+      constexpr int SPLIT_AT = VJ_GEMM_SPLIT_AT;  // m-tiles of the last phase before the B pieces
       if constexpr (!TAIL) {
-        if constexpr (SPREAD) {
-          if (VJ_GEMM_SPREAD == 1 && (DMAW == 8 || wave < DMAW))
+        if constexpr (SPREAD || SPREAD32) {
+          if ((SPREAD32 || VJ_GEMM_SPREAD == 1) && (DMAW == 8 || wave < DMAW))
             stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff, smem + sl * STAGE,
                                                  wave, lane);
         } else {
@@ -397,7 +406,17 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         mm8(Xb, 3, NTN / 2, NTN);
         __builtin_amdgcn_sched_barrier(0);
       } else if constexpr (BK == 32) {
-        mm(Ab, 1, Ba);
+        if constexpr (SPREAD32 && !TAIL) {
+          mm_rows(Ab, 1, Ba, 0, 2);
+          __builtin_amdgcn_sched_barrier(0);
+          if (DMAW == 8 || wave < DMAW)
+            stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
+                                                   smem + sl * STAGE + A_BYTES, wave, lane);
+          __builtin_amdgcn_sched_barrier(0);
+          mm_rows(Ab, 1, Ba, 2, 4);
+        } else {
+          mm(Ab, 1, Ba);
+        }
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < nk) {  // overwrite Aa / Ba once phase 1's MFMAs have been issued
           rdA(Aa, sl ^ 1, 0, 0);
@@ -420,14 +439,14 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           __builtin_amdgcn_sched_barrier(0);
           mm_rows(Ab, 1, Bb, 1, 2);
         } else {
-          mm_rows(Ab, 1, Bb, 0, 2);
+          mm_rows(Ab, 1, Bb, 0, SPLIT_AT);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (DMAW == 8 || wave < DMAW)
           stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
                                                  smem + sl * STAGE + A_BYTES, wave, lane);
         __builtin_amdgcn_sched_barrier(0);
-        mm_rows(Ab, 1, Bb, 2, 4);
+        mm_rows(Ab, 1, Bb, VJ_GEMM_SPREAD == 2 ? 2 : SPLIT_AT, 4);
       } else {
         mm(Ab, 1, Bb);
       }

@@ -44,6 +44,9 @@
 #ifndef VJ_ATTN_FWD_RING
 #define VJ_ATTN_FWD_RING 0
 #endif
+#ifndef VJ_ATTN_FWD_SPREAD
+#define VJ_ATTN_FWD_SPREAD 0
+#endif
 #ifndef VJ_ATTN_FWD_RING_V  // PV k-step after whose MFMAs the last two k-steps' V^T are read
 #define VJ_ATTN_FWD_RING_V 1
 #endif
@@ -435,7 +438,8 @@ void k_attn_fwd(AttnArgs a) {
     if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
       LDS_AS char* nx = smem + (cur ^ 1) * 2 * TB;
       stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
-      stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
+      // VJ_ATTN_FWD_SPREAD: the V tile after the S MFMAs (under the softmax) instead of in one burst
+      if (!VJ_ATTN_FWD_SPREAD) stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
     }
     f32x16 st[2];
 #pragma unroll
@@ -486,6 +490,11 @@ void k_attn_fwd(AttnArgs a) {
         vf[2][d] = tr_frag_at<HDP, VIMG, 32>(vlo[d], vhi[d]);
         vf[3][d] = tr_frag_at<HDP, VIMG, 48>(vlo[d], vhi[d]);
       }
+    }
+    if (VJ_ATTN_FWD_SPREAD && kt + 1 < nkt) {
+      __builtin_amdgcn_sched_barrier(0);
+      stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, smem + (cur ^ 1) * 2 * TB + TB, wave, lane, 4);
+      __builtin_amdgcn_sched_barrier(0);
     }
     const int kb = kt * KT;
     if (kb + KT > kmask0) {  // ragged last tile (or frame-causal boundary tiles): keys past the limit get -inf

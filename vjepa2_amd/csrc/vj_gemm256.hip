@@ -24,7 +24,8 @@
 // 8-wave main loop: the next K-tile's DMA pieces issued between the last phase's MFMAs instead of in
 // one burst after the barrier (1: B pieces halfway; 2: A pieces after the first quarter as well).
 // Measured (tools/bench_kernels.py, profiles/r03_gemm_spread_kernels.txt): 1 = -2..-7 % on the
-// ViT-L forward / data-gradient shapes.
+// ViT-L forward / data-gradient shapes; the B pieces after 3 of the phase's 4 m-tiles (SPLIT_AT 3)
+// a further 0..-5 % (r03_gemm_split_kernels.txt); spreading the 2W kernel's pieces did not pay.
 #ifndef VJ_GEMM_SPREAD
 #define VJ_GEMM_SPREAD 1
 #endif
@@ -32,7 +33,7 @@
 #define VJ_GEMM_SPREAD32 0
 #endif
 #ifndef VJ_GEMM_SPLIT_AT
-#define VJ_GEMM_SPLIT_AT 2
+#define VJ_GEMM_SPLIT_AT 3
 #endif
 
 namespace {

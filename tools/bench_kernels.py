@@ -108,6 +108,35 @@ def gemm_case(lib, case, dev, stream):
     return run, 2.0 * M * N * K
 
 
+# (name, M, ids_mod): fused QKV + RoPE GEMM (vj_qkv_rope_gemm) at the ViT-L target / context sizes,
+# 16 heads of 64, K = 1024; tokens by position (row % ids_mod: 8 frames x 16 x 16)
+ROPE = [("qkv rope tgt", 49152, 2048), ("qkv rope ctx", 11712, 2048)]
+
+
+def rope_case(lib, M, ids_mod, dev, stream):
+    import math
+    H, hd, K = 16, 64, 1024
+    N = 3 * H * hd
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = ((torch.rand(M, K, generator=g) * 2 - 1)).to(dev).bfloat16()
+    w = ((torch.rand(N, K, generator=g) * 2 - 1) * 0.05).to(dev).bfloat16()
+    b = torch.zeros(N, device=dev)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    half = (hd // 3) // 2
+    npos = 16
+    pos = torch.arange(npos, dtype=torch.float64)[:, None]
+    om = 1.0 / 10000 ** (torch.arange(half, dtype=torch.float64) / half)
+    cos_t = torch.cos(pos * om).float().to(dev).contiguous()
+    sin_t = torch.sin(pos * om).float().to(dev).contiguous()
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def run():
+        rc = lib.vj_qkv_rope_gemm(M, K, p(x), K, p(w), K, p(b), p(out), N, H, hd, None, ids_mod, 256, 16, p(cos_t),
+                                  p(sin_t), npos, stream)
+        assert rc == 0, rc
+    return run, 2.0 * M * N * K
+
+
 def attn_case(lib, hd, H, groups, dev, stream, bwd):
     T = sum(n * l for n, l in groups)
     D = H * hd
@@ -238,6 +267,10 @@ def main():
         if (only and only not in c[0]) or kind not in ("", "gemm"):
             continue
         cases.append((c[0], [gemm_case(lib, c, dev, stream) for lib in libs]))
+    for name, M, mod in ROPE:
+        if (only and only not in name) or kind not in ("", "gemm", "rope"):
+            continue
+        cases.append((name, [rope_case(lib, M, mod, dev, stream) for lib in libs]))
     for name, hd, H, groups, bwd in ATTN:
         if (only and only not in name) or kind not in ("", "attn"):
             continue

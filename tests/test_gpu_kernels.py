@@ -429,6 +429,11 @@ def test_fused_rope_paths(M, hd, H, monkeypatch):
             monkeypatch.setenv("VJ_GEMM_PP", pp)
             other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
             assert torch.equal(fused, other), f"qkv_rope: VJ_GEMM_PP={pp} differs from the default kernel"
+        for bm in ("1", "0"):  # 192-row tiles (where N takes 256-wide ones) == 256-row tiles, bitwise
+            monkeypatch.setenv("VJ_GEMM_BM192", bm)
+            other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
+            assert torch.equal(fused, other), f"qkv_rope: VJ_GEMM_BM192={bm} differs from the default kernel"
+        monkeypatch.delenv("VJ_GEMM_BM192")
         monkeypatch.setenv("VJ_GEMM_PP", "2")  # 32x32x16 form: other K order, one bf16 rounding apart
         other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
         _close(other, fused, 1e-3, 8e-3, "qkv_rope VJ_GEMM_PP=2 vs default")
@@ -723,6 +728,52 @@ def test_gemm_pingpong_matches_one_tile_kernel(K, pxcd, monkeypatch):
             assert frac < 0.05, f"pp32 {k}: {frac:.3f} of the bf16 outputs differ from the one-tile kernel"
         assert torch.equal(p32["gelu_a"], p32["gelu_nosave"])
         _close(p32["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "pp32 EPI_F32 vs fp32")
+
+
+@pytest.mark.parametrize("K", [64, 128, 1024])
+@pytest.mark.parametrize("pxcd", [None, "1"])
+def test_gemm_192_row_tiles_match_256(K, pxcd, monkeypatch):
+    """192-row tiles (k_gemm256<..., 192>: 3 m-tiles per wave M-half, chosen by the host cost model
+    for context-sized M) against the 256-row kernel on every direct-store epilogue: each output's K
+    order is the same sequence of MFMAs, so the outputs are BITWISE equal. M = 2100 / 1333 leave a
+    ragged last 192-row tile (and 256-row tile), K = 64 / 128 one / two K-tiles per tile,
+    VJ_GEMM_PXCD = 1 many tiles per block (the next tile's stages DMA'd under the epilogue)."""
+    from vjepa2_amd import ops
+
+    if pxcd:
+        monkeypatch.setenv("VJ_GEMM_PXCD", pxcd)
+    g = torch.Generator(device="cpu").manual_seed(K + 192)
+    for M, N in [(2100, 512), (1333, 1024)]:
+        X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+        W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
+        b = torch.randn(N, generator=g).to(DEV)
+        resid = torch.randn(M, N, generator=g).to(DEV)
+        dgs = torch.randn(M, N, generator=g).to(DEV).bfloat16()
+
+        def run():
+            outs = {"bf16": ops.linear_fwd(X, W, b, ops.EPI_BF16),
+                    "f32": ops.linear_fwd(X, W, b, ops.EPI_F32),
+                    "f32_resid": ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid),
+                    "bf16_resid": ops.linear_fwd(X, W, b, ops.EPI_BF16_RESID, resid=resid.bfloat16())}
+            d, a = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
+            outs["gelu_d"], outs["gelu_a"] = d, a
+            outs["gelu_nosave"] = ops.linear_fwd(X, W, b, ops.EPI_GELU)[1]
+            gb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(M, N, K, X, K, True, W, K, True, ops.EPI_GELU_BWD, out=gb, ldc=N, aux=dgs, ldaux=N)
+            outs["gelu_bwd"] = gb
+            torch.cuda.synchronize()
+            return {k: v.detach().clone() for k, v in outs.items()}
+
+        monkeypatch.setenv("VJ_GEMM_BM192", "1")
+        t192 = run()
+        monkeypatch.setenv("VJ_GEMM_BM192", "0")
+        t256 = run()
+        monkeypatch.delenv("VJ_GEMM_BM192")
+        for k in t192:
+            assert torch.equal(t192[k], t256[k]), f"192-row != 256-row tiles: {k} M={M} N={N} K={K} pxcd={pxcd}"
+        ref = X.float() @ W.float().t() + b
+        _close(t192["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "192-row EPI_F32")
+        assert torch.equal(t192["gelu_a"], t192["gelu_nosave"])
 
 
 def test_transpose_bf16_single_and_batched():

@@ -46,11 +46,16 @@ __device__ long vj_gemm_stamps[2048 * 16 * 4];
 // NWV = 8: 8 waves (2 x 4), 64-deep K tiles, one workgroup per CU. NWV = 4 ("2W"): 4 waves (2 x 2),
 // 32-deep K tiles, 64 KB of LDS, TWO workgroups per CU, so one workgroup's epilogue (HBM / VALU)
 // runs under the other's main loop (MFMA); K-major operands only.
-template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8>
+// BMT = 192 (8-wave, K-major bf16, 256-wide direct-store tiles only): 96-row wave tiles (3 m-tiles
+// per M-half) for problems whose 256-row tile count leaves a round of CUs under-filled (context
+// GEMMs, M ~ 11.7k: 184 tiles of 256 x 256 on 256 CUs -> 244 tiles of 192 x 256).
+template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256>
 __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   static_assert(!F8 || (AK && BKM && EPI != EPI_PARTIAL && EPI != EPI_GELU_BWD), "fp8: forward GEMMs only");
   static_assert(NWV == 8 || (NWV == 4 && AK && BKM && !F8), "2-workgroup GEMM: K-major bf16 operands only");
-  constexpr int BM = 256;
+  constexpr int BM = BMT;
+  constexpr int MH = BM / 64;     // m-tiles per M-half of a wave (4 / 3)
+  constexpr int WM = BM / 2;      // wave tile rows (128 / 96)
   constexpr int BK = NWV == 8 ? 64 : 32;
   constexpr int NT = NWV * 64;
   constexpr int WNX = NWV / 2;    // waves across N (4 / 2); 2 waves across M
@@ -63,6 +68,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // K-major B with 4 n-tiles per wave: permuted B staging + stores straight from registers (16-B
   // f32 / 8-B bf16 per row); 128-wide tiles would store 4-8 B per lane, so they keep the LDS path
   constexpr bool DIRECT = BKM && NTN == 4;
+  static_assert(BMT == 256 || (BMT == 192 && NWV == 8 && !F8 && AK && DIRECT), "192-row tiles: 8-wave direct K-major bf16");
   constexpr bool AUX = EPI == EPI_F32_RESID || EPI == EPI_GELU_BWD || EPI == EPI_BF16_RESID;
   constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_F32_RESID || EPI == EPI_PARTIAL;
 
@@ -178,13 +184,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
 #endif
 
-  f32x4 acc[8][NTN];
-  bf16x8 Aa[4], Ab[4], Ba[NTN], Bb[NTN];
+  f32x4 acc[2 * MH][NTN];
+  bf16x8 Aa[MH], Ab[MH], Ba[NTN], Bb[NTN];
   // A fragments of M-half mh (4 m-tiles), k-step ks; B fragments of all NTN n-tiles, k-step ks
-  auto rdA = [&](bf16x8 (&X)[4], int slot, int mh, int ks) {
+  auto rdA = [&](bf16x8 (&X)[MH], int slot, int mh, int ks) {
     const LDS_AS char* s = smem + slot * STAGE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) X[i] = frag<AK, BM, BK>(s, wr * 128 + (mh * 4 + i) * 16, ks, lane);
+    for (int i = 0; i < MH; ++i) X[i] = frag<AK, BM, BK>(s, wr * WM + (mh * MH + i) * 16, ks, lane);
   };
   auto rdB = [&](bf16x8 (&Y)[NTN], int slot, int ks) {
     const LDS_AS char* s = smem + slot * STAGE + A_BYTES;
@@ -226,32 +232,32 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         acc[2 * qq + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(X[i], Y8[j], acc[2 * qq + i][j], 0, 0,
                                                                               0, f8sa[2 * qq + i], 0, f8sb[j]);
   };
-  auto mm = [&](const bf16x8 (&X)[4], int mh, const bf16x8 (&Y)[NTN]) {
+  auto mm = [&](const bf16x8 (&X)[MH], int mh, const bf16x8 (&Y)[NTN]) {
 #if VJ_GEMM_PRIO
     __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MH; ++i)
 #pragma unroll
       for (int j = 0; j < NTN; ++j)
-        acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * 4 + i][j], 0, 0, 0);
+        acc[mh * MH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * MH + i][j], 0, 0, 0);
 #if VJ_GEMM_PRIO
     __builtin_amdgcn_s_setprio(0);
 #endif
   };
   // m-tiles i0 .. i1 - 1 of one phase (SPREAD splits the last phase around the B DMA pieces)
-  auto mm_rows = [&](const bf16x8 (&X)[4], int mh, const bf16x8 (&Y)[NTN], int i0, int i1) {
+  auto mm_rows = [&](const bf16x8 (&X)[MH], int mh, const bf16x8 (&Y)[NTN], int i0, int i1) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MH; ++i)
       if (i >= i0 && i < i1)
 #pragma unroll
         for (int j = 0; j < NTN; ++j)
-          acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * 4 + i][j], 0, 0, 0);
+          acc[mh * MH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * MH + i][j], 0, 0, 0);
   };
   // MN-major operands are read with asm transposed reads (ds_read_tr16_async): each phase first
   // waits for the fragments it consumes (read in the previous phase), then issues the next reads.
   constexpr bool ASYNC = !AK || !BKM;
-  auto release = [&](bf16x8 (&X)[4], bf16x8 (&Y)[NTN]) {
+  auto release = [&](bf16x8 (&X)[MH], bf16x8 (&Y)[NTN]) {
     if constexpr (ASYNC) {
       lds_wait();
       tie(X);
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       if (t < BM && cur.m0 + t < g.M) pf_id = g.rope.ids ? g.rope.ids[cur.m0 + t] : (cur.m0 + t) % g.rope.mod;
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 2 * MH; ++i)
 #pragma unroll
       for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (F8) {  // this tile's per-row scale exponents (retired by the wait below)
@@ -374,7 +380,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       constexpr bool SPREAD = VJ_GEMM_SPREAD && NWV == 8 && !F8 && BK == 64;
       // the same for the two-workgroup kernel's 32-deep K-tiles (one phase after the barrier)
       constexpr bool SPREAD32 = VJ_GEMM_SPREAD32 && NWV == 4 && BK == 32;
-      constexpr int SPLIT_AT = VJ_GEMM_SPLIT_AT;  // m-tiles of the last phase before the B pieces
+      constexpr int SPLIT_AT = MH == 4 ? VJ_GEMM_SPLIT_AT : MH - 1;  // m-tiles of the last phase before the B pieces
       if constexpr (!TAIL) {
         if constexpr (SPREAD || SPREAD32) {
           if ((SPREAD32 || VJ_GEMM_SPREAD == 1) && (DMAW == 8 || wave < DMAW))
@@ -447,7 +453,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
                                                  smem + sl * STAGE + A_BYTES, wave, lane);
         __builtin_amdgcn_sched_barrier(0);
-        mm_rows(Ab, 1, Bb, VJ_GEMM_SPREAD == 2 ? 2 : SPLIT_AT, 4);
+        mm_rows(Ab, 1, Bb, VJ_GEMM_SPREAD == 2 ? 2 : SPLIT_AT, MH);
       } else {
         mm(Ab, 1, Bb);
       }
@@ -470,7 +476,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     if (true) {
       float sum = 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 2 * MH; ++i)
 #pragma unroll
         for (int j = 0; j < NTN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
       if (sum == 1.2345e-30f && g.C) ((float*)g.C)[lane_e] = sum;
@@ -488,7 +494,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // out of registers as one 8/16-B store; no LDS round trip.
       const int nb = cur.n0 + wc * WN + NTN * (lane & 15);
       const bool nok = nb < g.N;
-      const int mb = cur.m0 + wr * 128 + 4 * (lane >> 4);
+      const int mb = cur.m0 + wr * WM + 4 * (lane >> 4);
       float bias[NTN];
 #pragma unroll
       for (int j = 0; j < NTN; ++j) bias[j] = 0.f;
@@ -583,10 +589,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       auto rows = [&](auto save_c) {
       constexpr bool SAVE_D = decltype(save_c)::value;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 2 * MH; ++i) {
         if constexpr (AUX) {
-          if (i + AUX_PF < 8) fetch(i + AUX_PF, aux[(i + AUX_PF) % (AUX_PF + 1)]);
-          if (i == 7 - AUX_PF && has_next) {  // behind the last aux fetch
+          if (i + AUX_PF < 2 * MH) fetch(i + AUX_PF, aux[(i + AUX_PF) % (AUX_PF + 1)]);
+          if (i == 2 * MH - 1 - AUX_PF && has_next) {  // behind the last aux fetch
             const Tile nxt = make_tile(wgn);
             if (nxt.nk > 1) load_tile(nxt, 1, sle, lane);
           }
@@ -636,7 +642,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
 #pragma unroll
           for (int j = 0; j < NTN; ++j) v[j] = acc[i][j][r] + bias[j];
           if constexpr (EPI == EPI_ROPE) {
-            const int rp = rpos[wr * 128 + i * 16 + 4 * (lane >> 4) + r];
+            const int rp = rpos[wr * WM + i * 16 + 4 * (lane >> 4) + r];
 #pragma unroll
             for (int p = 0; p < NTN / 2; ++p) {
               if (!ract[p]) continue;
@@ -922,6 +928,40 @@ int launch2w(int epi, G256 g, hipStream_t st) {
   return VJ_OK;
 }
 
+// one-tile launch; 192-row tiles (BMT = 192) for the K-major 256-wide shapes vm192() picks
+int launch192(int epi, const G256& g, hipStream_t st) {
+  const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
+  const_cast<G256&>(g).stagger = stagger_units(g.kslice);
+#define L192(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 192>), grid, dim3(512), 0, st, g); break
+  switch (epi) {
+    case EPI_BF16: L192(EPI_BF16);
+    case EPI_F32: L192(EPI_F32);
+    case EPI_F32_RESID: L192(EPI_F32_RESID);
+    case EPI_GELU: L192(EPI_GELU);
+    case EPI_GELU_BWD: L192(EPI_GELU_BWD);
+    case EPI_ROPE: L192(EPI_ROPE);
+    case EPI_BF16_RESID: L192(EPI_BF16_RESID);
+    default: vj_set_error("gemm192: bad epilogue %d", epi); return VJ_ERR_ARG;
+  }
+#undef L192
+  VJ_LAUNCH_CHECK("vj_gemm256(192)");
+  return VJ_OK;
+}
+
+// Tile rows for a K-major 256-wide GEMM: 192 when its rounds of tiles over the CUs cost less than
+// with 256 rows (rounds x rows, 192-row tiles charged 8 % for their lower MFMA : fragment-read ratio).
+// Context GEMMs (M ~ 11.7k, N = 1024 / 3072) take 192; the target / predictor shapes fill the CUs at
+// 256. VJ_GEMM_BM192: 0 = never, 1 = always, unset = the cost model.
+bool use_bm192(int M, int tn) {
+  const char* e = getenv("VJ_GEMM_BM192");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  const long cus = num_cus();
+  const long r256 = ((long)vj_cdiv(M, 256) * tn + cus - 1) / cus;
+  const long r192 = ((long)vj_cdiv(M, 192) * tn + cus - 1) / cus;
+  return r192 * 192 * 108 < r256 * 256 * 100;
+}
+
 template <bool AK, bool BKM, int BN>
 int launch256(int epi, const G256& g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n * g.nsplit));
@@ -995,6 +1035,11 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
     return launch2w(epi, g, st);
   }
   if (bn == 256) {
+    if (a_kmajor && b_kmajor && use_bm192(M, tn)) {
+      g.tiles_m = vj_cdiv(M, 192);
+      g.group = tile_group(g.tiles_m, tn);
+      return launch192(epi, g, st);
+    }
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
     if (a_kmajor && !b_kmajor) return launch256<true, false, 256>(epi, g, st);
     if (!a_kmajor && b_kmajor) return launch256<false, true, 256>(epi, g, st);

@@ -948,10 +948,12 @@ int launch192(int epi, const G256& g, hipStream_t st) {
   return VJ_OK;
 }
 
-// Tile rows for a K-major 256-wide GEMM: 192 when its rounds of tiles over the CUs cost less than
-// with 256 rows (rounds x rows, 192-row tiles charged 8 % for their lower MFMA : fragment-read ratio).
-// Context GEMMs (M ~ 11.7k, N = 1024 / 3072) take 192; the target / predictor shapes fill the CUs at
-// 256. VJ_GEMM_BM192: 0 = never, 1 = always, unset = the cost model.
+// Tile rows for a K-major 256-wide GEMM: 192 when its rounds of tiles over the CUs cost clearly less
+// than with 256 rows: rounds x rows, 192-row tiles charged 8 % for their lower MFMA : fragment-read
+// ratio (measured 6-9 % on full-round shapes), and at least 15 % predicted gain (a predictor step
+// whose M made the 8 % rule pick 192 ran its fc1 / dgrad slower). Context GEMMs (M ~ 11.7k,
+// N = 1024 / 3072) take 192; the target / predictor shapes keep 256. VJ_GEMM_BM192: 0 = never,
+// 1 = always, unset = the cost model.
 bool use_bm192(int M, int tn) {
   const char* e = getenv("VJ_GEMM_BM192");
   if (e && e[0] == '0') return false;
@@ -959,7 +961,7 @@ bool use_bm192(int M, int tn) {
   const long cus = num_cus();
   const long r256 = ((long)vj_cdiv(M, 256) * tn + cus - 1) / cus;
   const long r192 = ((long)vj_cdiv(M, 192) * tn + cus - 1) / cus;
-  return r192 * 192 * 108 < r256 * 256 * 100;
+  return r192 * 192 * 108 < r256 * 256 * 85;
 }
 
 template <bool AK, bool BKM, int BN>

@@ -41,6 +41,12 @@
 
 // forward workgroups per CU the register budget is sized for (head dims <= 64)
 // forward, head dim 64: K / V^T fragments in rings (fewer live registers) at 4 workgroups per CU
+#ifndef VJ_ATTN_PRIO  // forward: s_setprio 1 around the S and PV MFMA clusters
+#define VJ_ATTN_PRIO 3
+#endif
+#ifndef VJ_ATTN_BPRIO  // backward sweeps: s_setprio 1 around the S / dP (bit 0) and dV / dK or dQ (bit 1) MFMAs
+#define VJ_ATTN_BPRIO 0
+#endif
 #ifndef VJ_ATTN_FWD_RING
 #define VJ_ATTN_FWD_RING 0
 #endif
@@ -429,6 +435,10 @@ void k_attn_fwd(AttnArgs a) {
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
   stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
   __syncthreads();
+  // VJ_ATTN_PRIO (head dim 64): s_setprio 1 around the S (bit 0) / PV (bit 1) MFMA clusters, so a
+  // wave's MFMA chain keeps the issue arbitration over the other waves' softmax VALU
+  constexpr bool PRIO_S = HD == 64 && (VJ_ATTN_PRIO & 1);
+  constexpr bool PRIO_PV = HD == 64 && (VJ_ATTN_PRIO & 2);
   // loop body with the LDS buffer index as a compile-time constant (unrolled by 2), so every LDS
   // address is a per-lane base register plus an immediate offset
   auto tile_iter = [&](const int kt, auto cur_c) {
@@ -476,11 +486,13 @@ void k_attn_fwd(AttnArgs a) {
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int s = 0; s < HDP / 16; ++s) kf[kk][s] = row_frag<HDP>(Ks, kk * 32, s, lane);
+      if (PRIO_S) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
           st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][s], qf[s], st[kk], 0, 0, 0);
+      if (PRIO_S) __builtin_amdgcn_s_setprio(0);
       // V^T fragments: issued before the softmax so their LDS latency hides under it (per-lane base
       // registers + immediates: the buffer and the k-step are compile-time)
 #pragma unroll
@@ -563,12 +575,14 @@ void k_attn_fwd(AttnArgs a) {
     } else {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) tie(vf[ks]);
+      if (PRIO_PV) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
 #pragma unroll
         for (int d = 0; d < HDP / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
       }
+      if (PRIO_PV) __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
   };
@@ -786,6 +800,7 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
         if (qt > qt_first) dq_tile(qt - 1, dsimg + (cur ^ 1) * DSB);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if (VJ_ATTN_BPRIO & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
@@ -793,6 +808,7 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
           sacc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[kw][s], sacc[kw], 0, 0, 0);
           dp[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[kw][s], dp[kw], 0, 0, 0);
         }
+      if (VJ_ATTN_BPRIO & 1) __builtin_amdgcn_s_setprio(0);
     } else {
       // This tile's S / dP MFMAs interleaved with the previous tile's fused dQ product: dQ chunk c
       // (two 32-key steps of one 16x16 block) is read from LDS one step ahead, into alternating
@@ -892,6 +908,7 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
       tie(dtf[s2]);
       tie(qtf[s2]);
     }
+    if (VJ_ATTN_BPRIO & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -904,6 +921,7 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
           dkt[kw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtf[s2][d], sf, dkt[kw][d], 0, 0, 0);
         }
       }
+    if (VJ_ATTN_BPRIO & 2) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
   };
   for (int qt0 = qt_first; qt0 < nqt; qt0 += 2) {
@@ -1065,6 +1083,7 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
           st[qw][r] = nl2[qw];
           dpt[qw][r] = dl[qw];
         }
+      if (VJ_ATTN_BPRIO & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
@@ -1072,6 +1091,7 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
           st[qw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s], qf[qw][s], st[qw], 0, 0, 0);
           dpt[qw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s], gf[qw][s], dpt[qw], 0, 0, 0);
         }
+      if (VJ_ATTN_BPRIO & 1) __builtin_amdgcn_s_setprio(0);
       // keys past the end are zero rows of K and V; masked on the ragged last tile only so an
       // extreme lse cannot turn 2^(-lse2) * 0 into inf * 0
       if (ragged) {  // uniform branch, last tile only
@@ -1089,6 +1109,7 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
       lds_wait();
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) tie(ktf[s2]);
+      if (VJ_ATTN_BPRIO & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -1098,6 +1119,7 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
           for (int d = 0; d < HDP / 32; ++d)
             dqt[qw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktf[s2][d], sf, dqt[qw][d], 0, 0, 0);
         }
+      if (VJ_ATTN_BPRIO & 2) __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
   };

@@ -9,3 +9,6 @@ for r in 1 2; do
     python3 -c "import json; d=json.loads([l for l in open('$o/bench_${b}_$r.log') if l.startswith('{')][-1]); print('$b run $r', d['value'], d['ms_per_step'], d['ms_per_step_median'])"
   done
 done
+# GEMM: s_setprio around each phase's MFMAs (gprio) / static priority for waves 4-7 (gsprio)
+VJ_BENCH_KIND=gemm VJ_BENCH_ROUNDS=7 timeout -k 10 300 python -u tools/bench_kernels.py vjepa2_amd/libvjepa_hip.so vjepa2_amd/libvjepa_hip_gprio.so vjepa2_amd/libvjepa_hip_gsprio.so > $o/bk.log 2>&1 || { echo "bench failed"; tail -5 $o/bk.log; exit 3; }
+cat $o/bk.log

@@ -295,7 +295,8 @@ def _pmc_traffic(label, workload):
         return None
     for tr in data if isinstance(data, list) else [data]:  # one entry per (kernel, workload)
         if tr.get("kernel") == label and tr.get("workload", "vit_large 16x256^2 B=24") == workload:
-            tr["source"] = "profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py)"
+            tr["source"] = ("profiles/traffic.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over bench.py; "
+                            "L2-to-fabric bytes, Infinity-Cache hits included, so an upper bound on HBM bytes)")
             return tr
     return None
 

@@ -64,7 +64,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int WN = BN / WNX;    // wave tile columns (64 / 32)
   constexpr int NTN = WN / 16;    // 16-wide n tiles per wave (4 / 2)
-  constexpr int DMAW = NWV == 8 ? VJ_GEMM_DMA_WAVES : NWV;
+  // LDS-DMA issuers: VJ_GEMM_DMA_WAVES = 4 -> waves 0-3 only on 256-wide tiles (their SIMD partners
+  // 4-7 keep issuing MFMAs meanwhile), except the RoPE / GELU / GELU-backward tiles, whose next-tile
+  // stage 1 goes out right before (or in) their VALU-heavy epilogue, where waves 0-3 would start it
+  // 16 pieces late; 128-wide tiles (the predictor's N = 384) measured slower with it. 8 = all waves.
+  constexpr bool VALU_EPI = EPI == EPI_ROPE || EPI == EPI_GELU || EPI == EPI_GELU_BWD;
+  constexpr int DMAW = NWV != 8 ? NWV : (VJ_GEMM_DMA_WAVES == 8 || VALU_EPI || BN != 256 || F8) ? 8 : VJ_GEMM_DMA_WAVES;
   // K-major B with 4 n-tiles per wave: permuted B staging + stores straight from registers (16-B
   // f32 / 8-B bf16 per row); 128-wide tiles would store 4-8 B per lane, so they keep the LDS path
   constexpr bool DIRECT = BKM && NTN == 4;

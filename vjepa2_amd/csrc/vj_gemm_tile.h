@@ -13,9 +13,11 @@ namespace {
 #define VJ_GEMM_AUX_PF 1
 #endif
 // Waves that issue the LDS-DMA of a K stage: 8 (all) or 4 (waves 0-3, so their SIMD partners 4-7
-// keep the matrix pipe busy while the DMA issues)
+// keep the matrix pipe busy while the DMA issues; k_gemm256 applies it to its 256-wide bf16 tiles
+// without a VALU-heavy epilogue). Measured (profiles/r03_gemm_dmaw4_kernels.txt): those shapes
+// -1.5..-7 %, step +0.1..0.3 % (three same-call A/Bs).
 #ifndef VJ_GEMM_DMA_WAVES
-#define VJ_GEMM_DMA_WAVES 8
+#define VJ_GEMM_DMA_WAVES 4
 #endif
 
 // EPI_BF16_RESID: bf16 residual in (aux), bf16 out — the no-grad target encoder's residual stream in

@@ -35,6 +35,14 @@
 #ifndef VJ_GEMM_SPLIT_AT
 #define VJ_GEMM_SPLIT_AT 3
 #endif
+// VJ_GEMM_DMA8_S1 = 1: the RoPE / GELU / GELU-backward tiles also take the waves-0-3 DMA in their main
+// loop (the next tile's stage 1, issued around the epilogue, always goes out from all 8 waves)
+#ifndef VJ_GEMM_DMA8_S1
+#define VJ_GEMM_DMA8_S1 0
+#endif
+#ifndef VJ_GEMM_S1_ALL  // 0: the next tile's stage 1 from the DMA-issuing waves only (as the main loop)
+#define VJ_GEMM_S1_ALL 1
+#endif
 
 namespace {
 
@@ -69,7 +77,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // stage 1 goes out right before (or in) their VALU-heavy epilogue, where waves 0-3 would start it
   // 16 pieces late; 128-wide tiles (the predictor's N = 384) measured slower with it. 8 = all waves.
   constexpr bool VALU_EPI = EPI == EPI_ROPE || EPI == EPI_GELU || EPI == EPI_GELU_BWD;
-  constexpr int DMAW = NWV != 8 ? NWV : (VJ_GEMM_DMA_WAVES == 8 || VALU_EPI || BN != 256 || F8) ? 8 : VJ_GEMM_DMA_WAVES;
+  constexpr int DMAW = NWV != 8 ? NWV : (VJ_GEMM_DMA_WAVES == 8 || (VALU_EPI && !VJ_GEMM_DMA8_S1) || BN != 256 || F8) ? 8 : VJ_GEMM_DMA_WAVES;
   // K-major B with 4 n-tiles per wave: permuted B staging + stores straight from registers (16-B
   // f32 / 8-B bf16 per row); 128-wide tiles would store 4-8 B per lane, so they keep the LDS path
   constexpr bool DIRECT = BKM && NTN == 4;
@@ -155,6 +163,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   };
   auto load_tile = [&](const Tile& T, int t, int slot, int lane) {
     load_k(rsrc_a(T), rsrc_b(T), T, t, slot, lane);
+  };
+  // the next tile's stage 1, issued around the epilogue (no MFMAs to keep fed): all 8 waves
+  auto load_tile8 = [&](const Tile& T, int t, int slot, int lane) {
+    if (!VJ_GEMM_S1_ALL) return load_tile(T, t, slot, lane);
+    LDS_AS char* s = smem + slot * STAGE;
+    stage<AK, BM, false, NWV, BK, WNX>(rsrc_a(T), g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
+    stage<BKM, BN, DIRECT, NWV, BK, WNX>(rsrc_b(T), g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, wave, lane);
   };
 
   // per-kernel tables (RoPE): global loads issued before the first DMA (so their waits do not queue
@@ -404,7 +419,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           load_tile(nx, 0, sl, lt);
         } else {
           if (nk == 1) load_tile(nx, 0, sl ^ 1, lt);
-          if (EARLY1 && nx.nk > 1) load_tile(nx, 1, sl, lt);
+          if (EARLY1 && nx.nk > 1) load_tile8(nx, 1, sl, lt);
         }
       }
       if constexpr (F8) {
@@ -599,7 +614,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           if (i + AUX_PF < 2 * MH) fetch(i + AUX_PF, aux[(i + AUX_PF) % (AUX_PF + 1)]);
           if (i == 2 * MH - 1 - AUX_PF && has_next) {  // behind the last aux fetch
             const Tile nxt = make_tile(wgn);
-            if (nxt.nk > 1) load_tile(nxt, 1, sle, lane);
+            if (nxt.nk > 1) load_tile8(nxt, 1, sle, lane);
           }
         }
         if constexpr (F32OUT && NTN == 4) {
@@ -807,7 +822,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       __syncthreads();  // every wave is done with its image before the slot is DMA'd
       if (has_next) {
         const Tile nxt = make_tile(wgn);
-        if (nxt.nk > 1) load_tile(nxt, 1, sle, lane);
+        if (nxt.nk > 1) load_tile8(nxt, 1, sle, lane);
       }
     }
 

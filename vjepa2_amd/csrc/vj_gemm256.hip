@@ -40,6 +40,9 @@
 #ifndef VJ_GEMM_DMA8_S1
 #define VJ_GEMM_DMA8_S1 0
 #endif
+#ifndef VJ_GEMM_DMA_SPLIT  // 1: with 4 DMA waves, A pieces from waves 0-3 and B pieces from waves 4-7
+#define VJ_GEMM_DMA_SPLIT 0
+#endif
 #ifndef VJ_GEMM_S1_ALL  // 0: the next tile's stage 1 from the DMA-issuing waves only (as the main loop)
 #define VJ_GEMM_S1_ALL 1
 #endif
@@ -153,13 +156,16 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     return make_rsrc(bbase, BKM ? clampb((long)(g.N - T.n0) * g.ldb * 2 - kb * 2L)
                                 : clampb(((long)(g.K - kb) * g.ldb - T.n0) * 2));
   };
+  // DSPLIT (VJ_GEMM_DMA_SPLIT, with 4 DMA waves): A pieces from waves 0-3, B pieces from waves 4-7
+  constexpr bool DSPLIT = VJ_GEMM_DMA_SPLIT && NWV == 8 && DMAW == 4;
+  const bool a_iss = DMAW == 8 || wave < DMAW;
+  const bool b_iss = DSPLIT ? wave >= 4 : a_iss;
+  const int bwv = DSPLIT ? wave - 4 : wave;
   auto load_k = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, const Tile& T, int t, int slot,
                     int lane) {
-    if (DMAW == 8 || wave < DMAW) {
-      LDS_AS char* s = smem + slot * STAGE;
-      stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
-      stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, wave, lane);
-    }
+    LDS_AS char* s = smem + slot * STAGE;
+    if (a_iss) stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
+    if (b_iss) stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, bwv, lane);
   };
   auto load_tile = [&](const Tile& T, int t, int slot, int lane) {
     load_k(rsrc_a(T), rsrc_b(T), T, t, slot, lane);
@@ -403,7 +409,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       constexpr int SPLIT_AT = MH == 4 ? VJ_GEMM_SPLIT_AT : MH - 1;  // m-tiles of the last phase before the B pieces
       if constexpr (!TAIL) {
         if constexpr (SPREAD || SPREAD32) {
-          if ((SPREAD32 || VJ_GEMM_SPREAD == 1) && (DMAW == 8 || wave < DMAW))
+          if ((SPREAD32 || VJ_GEMM_SPREAD == 1) && a_iss)
             stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff, smem + sl * STAGE,
                                                  wave, lane);
         } else {
@@ -469,9 +475,9 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           mm_rows(Ab, 1, Bb, 0, SPLIT_AT);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (DMAW == 8 || wave < DMAW)
+        if (b_iss)
           stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
-                                                 smem + sl * STAGE + A_BYTES, wave, lane);
+                                                 smem + sl * STAGE + A_BYTES, bwv, lane);
         __builtin_amdgcn_sched_barrier(0);
         mm_rows(Ab, 1, Bb, VJ_GEMM_SPREAD == 2 ? 2 : SPLIT_AT, MH);
       } else {

@@ -43,6 +43,9 @@
 #ifndef VJ_GEMM_DMA_SPLIT  // 1: with 4 DMA waves, A pieces from waves 0-3 and B pieces from waves 4-7
 #define VJ_GEMM_DMA_SPLIT 0
 #endif
+#ifndef VJ_GEMM_DMA_HI  // 1: the 4 DMA-issuing waves are 4-7
+#define VJ_GEMM_DMA_HI 0
+#endif
 #ifndef VJ_GEMM_S1_ALL  // 0: the next tile's stage 1 from the DMA-issuing waves only (as the main loop)
 #define VJ_GEMM_S1_ALL 1
 #endif
@@ -158,13 +161,15 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   };
   // DSPLIT (VJ_GEMM_DMA_SPLIT, with 4 DMA waves): A pieces from waves 0-3, B pieces from waves 4-7
   constexpr bool DSPLIT = VJ_GEMM_DMA_SPLIT && NWV == 8 && DMAW == 4;
-  const bool a_iss = DMAW == 8 || wave < DMAW;
+  // VJ_GEMM_DMA_HI: the 4 DMA waves are 4-7 (the younger half) instead of 0-3
+  const int dwv = (VJ_GEMM_DMA_HI && NWV == 8 && DMAW == 4 && !DSPLIT) ? wave - 4 : wave;
+  const bool a_iss = DMAW == 8 || (dwv >= 0 && dwv < DMAW);
   const bool b_iss = DSPLIT ? wave >= 4 : a_iss;
-  const int bwv = DSPLIT ? wave - 4 : wave;
+  const int bwv = DSPLIT ? wave - 4 : dwv;
   auto load_k = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, const Tile& T, int t, int slot,
                     int lane) {
     LDS_AS char* s = smem + slot * STAGE;
-    if (a_iss) stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
+    if (a_iss) stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, dwv, lane);
     if (b_iss) stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, bwv, lane);
   };
   auto load_tile = [&](const Tile& T, int t, int slot, int lane) {
@@ -411,7 +416,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         if constexpr (SPREAD || SPREAD32) {
           if ((SPREAD32 || VJ_GEMM_SPREAD == 1) && a_iss)
             stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff, smem + sl * STAGE,
-                                                 wave, lane);
+                                                 dwv, lane);
         } else {
           load_k(ra, rb, cur, t + 2, sl, lane);
         }

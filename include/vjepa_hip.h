@@ -161,9 +161,10 @@ int vj_gather_rows(int R, int rowbytes, const void* src, long src_ld_bytes, cons
                    long dst_ld_bytes, int scatter, void* stream);
 /* dst[idx[r]] = vec (mask tokens, predictor.py:194-197). */
 int vj_fill_rows(int R, int D, float* dst, long ldd, const int* idx, const float* vec, void* stream);
-/* dst[r] += table[idx ? idx[r] : r % idx_mod] (sincos pos-embed add, non-RoPE variant). */
-int vj_add_rows(int R, int D, float* dst, long ldd, const float* table, long ldt, const int* idx, int idx_mod,
-                void* stream);
+/* dst[r] += table[idx ? idx[r] : r % idx_mod] (sincos pos-embed add, non-RoPE variant); table has
+ * trows rows: an id outside [0, trows) is not read and leaves its row unchanged. */
+int vj_add_rows(int R, int D, float* dst, long ldd, const float* table, long ldt, int trows, const int* idx,
+                int idx_mod, void* stream);
 
 /* Predictor sort indices for one mask pair: stable rank of cat(mx[b], my[b]) (= torch.argsort for
  * unique ids, predictor.py:210-217; inverse at :240-242). Outputs int32 (see vj_ops.hip). */

@@ -150,3 +150,54 @@ def test_inf_skip_does_not_advance_step():
     assert opt.steps == [2, 2, 2, 2]
     for n, p in named:
         torch.testing.assert_close(p.detach().cpu(), named_ref[n].detach(), rtol=2e-6, atol=2e-7, msg=n)
+
+
+def test_lazy_zero_overwrite_marked_grad_not_written_is_zero():
+    """FlatArena.zero_grad leaves the gradients of weights a weight-gradient GEMM overwrites
+    (functions.wgrad_buf marks them) untouched until their first write of the step. A marked weight
+    that nothing writes in a step (here: p1) must reach check_finite / AdamW as zeros, not as the
+    previous step's values; a marked weight first touched by an accumulating write (grad_buf) is
+    zeroed before it. Checked against torch AdamW fed the true gradients (p1: zero)."""
+    from vjepa2_amd.arena import FlatArena, FusedAdamW
+    from vjepa2_amd.functions import grad_buf, wgrad_buf
+
+    torch.manual_seed(3)
+    ps = [nn.Parameter(torch.randn(8, 16)) for _ in range(3)]
+    ref = [nn.Parameter(p.detach().clone()) for p in ps]
+    arena = FlatArena([(f"w{i}", p) for i, p in enumerate(ps)], DEV)
+    opt = FusedAdamW([arena], [None], lr=1e-2, weight_decay=0.04)
+    ropt = torch.optim.AdamW(ref, lr=1e-2, weight_decay=0.04)
+    g = torch.Generator().manual_seed(5)
+    # step 1: every weight written through the overwrite path (marks them)
+    g1 = [torch.randn(8, 16, generator=g) for _ in ps]
+    for p, gg in zip(ps, g1):
+        buf, acc = wgrad_buf(p)
+        assert not acc  # first write of the step overwrites
+        buf.copy_(gg)
+    for r, gg in zip(ref, g1):
+        r.grad = gg.clone()
+    opt.step(found_inf=opt.check_finite())
+    ropt.step()
+    opt.zero_grad()
+    assert all(getattr(p, "_vj_ow", False) for p in ps)
+    # step 2: p0 overwritten, p1 not written at all (stale step-1 values still in the arena), p2 first
+    # touched by an accumulating write (must start from zero), then by an overwrite-path call
+    g2 = [torch.randn(8, 16, generator=g) for _ in ps]
+    buf, acc = wgrad_buf(ps[0])
+    assert not acc
+    buf.copy_(g2[0])
+    grad_buf(ps[2]).add_(g2[2].to(DEV))
+    buf, acc = wgrad_buf(ps[2])
+    assert acc  # already touched this step: accumulate
+    buf.add_(g2[2].to(DEV))
+    found = opt.check_finite()  # finalize_grads zeroes p1
+    torch.cuda.synchronize()
+    assert int(found.item()) == 0
+    assert ps[1].grad.abs().max().item() == 0.0, "stale gradient of an unwritten overwrite-marked weight"
+    torch.testing.assert_close(ps[2].grad.cpu(), 2 * g2[2])
+    opt.step(found_inf=found)
+    ref[0].grad, ref[1].grad, ref[2].grad = g2[0].clone(), torch.zeros(8, 16), 2 * g2[2]
+    ropt.step()
+    torch.cuda.synchronize()
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p.detach().cpu(), r.detach(), rtol=2e-6, atol=2e-7)

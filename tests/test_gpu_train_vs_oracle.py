@@ -113,12 +113,27 @@ def test_two_fpc_groups_vs_oracle():
     gen = torch.Generator().manual_seed(1)
     clips = [torch.randn(B, 3, T, S, S, generator=gen) for T in (8, 4)]
     tok0 = [t.detach().cpu().clone() for t in tr.mask_tokens]
-    loss = tr.compute_grads([c.to(dev) for c in clips], [[m.to(dev) for m in g[1]] for g in groups],
-                            [[m.to(dev) for m in g[2]] for g in groups]).item()
-    torch.cuda.synchronize()
-    got = {("enc", k): p.grad.detach().cpu().clone() for k, p in enc.backbone.named_parameters()}
-    got.update({("pred", k): p.grad.detach().cpu().clone() for k, p in pred.backbone.named_parameters()
-                if p.grad is not None})
+    args = ([c.to(dev) for c in clips], [[m.to(dev) for m in g[1]] for g in groups],
+            [[m.to(dev) for m in g[2]] for g in groups])
+
+    def grads():
+        torch.cuda.synchronize()
+        d = {("enc", k): p.grad.detach().cpu().clone() for k, p in enc.backbone.named_parameters()}
+        d.update({("pred", k): p.grad.detach().cpu().clone() for k, p in pred.backbone.named_parameters()
+                  if p.grad is not None})
+        return d
+
+    # A first pass marks the weight-gradient outputs overwrite-on-first-write; after opt.zero_grad()
+    # they still hold this pass's values, so the measured pass runs the lazy-zero paths across groups
+    # (group 0 overwrites, group 1 accumulates). Its gradients must equal the first pass's bitwise.
+    loss0 = tr.compute_grads(*args).item()
+    first = grads()
+    opt.zero_grad()
+    loss = tr.compute_grads(*args).item()
+    got = grads()
+    assert loss == loss0
+    for key, gk in got.items():
+        assert torch.equal(gk, first[key]), f"{key}: gradient differs on the lazily zeroed pass"
     tr.apply_update(0.99925)
     ref = orc.OracleTrainer(enc_sd, pred_sd, dict(patch_size=16, tubelet_size=2, num_heads=6, depth=12, use_rope=True),
                             dict(num_heads=12, depth=2, use_rope=True, grid_size=S // 16, num_mask_tokens=4,

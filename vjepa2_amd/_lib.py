@@ -54,7 +54,7 @@ SIGNATURES = {
     "vj_im2col_tubelet": [_I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "vj_gather_rows": [_I, _I, _P, _L, _P, _P, _L, _I, _P],
     "vj_fill_rows": [_I, _I, _P, _L, _P, _P, _P],
-    "vj_add_rows": [_I, _I, _P, _L, _P, _L, _P, _I, _P],
+    "vj_add_rows": [_I, _I, _P, _L, _P, _L, _I, _P, _I, _P],
     "vj_pred_index": [_I, _I, _I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P],
     "vj_ids64to32": [_L, _P, _P, _P],
     "vj_jepa_loss": [_I, _I, _P, _I, _L, _P, _I, _L, _P, _P, _P, _F, _F, _F, _I, _P, _F, _P, _L, _P, _P, _P],

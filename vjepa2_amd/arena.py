@@ -98,7 +98,13 @@ class FlatArena:
         """Zero the gradients, lazily for the weights that a weight-gradient GEMM overwrites on its
         first write of a step (functions.wgrad_buf marks them): those keep their old values until
         then (no fill pass over ~1.3 GB of ViT-L gradients, and the GEMM epilogue does not read them
-        back). Every other gradient is zeroed here, in contiguous runs."""
+        back). Every other gradient is zeroed here, in contiguous runs.
+
+        Consequence for callers: between zero_grad() and finalize_grads() (run by compute_grads /
+        check_finite / step) the .grad of a marked weight is NOT valid (it holds the previous step's
+        values until its first write). Write such gradients only through functions.wgrad_buf /
+        grad_buf, which zero or overwrite on the first touch; an external `p.grad += ...` (e.g. a
+        torch AccumulateGrad) before that first touch would add onto stale data."""
         if self.grad is None:
             return
         self.epoch += 1

@@ -153,6 +153,12 @@ __device__ __forceinline__ uint32_t f8pack4(float a, float b, float c, float d) 
   return (uint32_t)w;
 }
 
+// GEMM epilogues: ONE numbering for every GEMM source (vj_gemm.hip, vj_gemm256.hip, vj_gemm_pp.hip,
+// vj_f32.hip) and the public header (include/vjepa_hip.h VJ_EPI_*). EPI_PARTIAL is internal (split-K
+// f32 partial slabs); EPI_BF16_RESID: bf16 residual in (aux), bf16 out.
+enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5, EPI_PARTIAL = 6,
+       EPI_BF16_RESID = 7 };
+
 static inline int vj_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // nn.GELU() (exact erf form, vision_transformer.py:100) and its derivative in one pass (the erf

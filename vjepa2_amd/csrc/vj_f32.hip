@@ -8,7 +8,7 @@
 
 namespace {
 
-enum { EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3 };  // numbering of vj_gemm_bf16's epilogues
+// epilogue numbering (EPI_F32, EPI_F32_RESID, EPI_GELU): vj_common.h, as vj_gemm_bf16's
 
 __device__ __forceinline__ int acc_row32(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 

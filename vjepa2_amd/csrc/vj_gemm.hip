@@ -23,7 +23,7 @@
 
 namespace {
 
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_PARTIAL = 5, EPI_BF16_RESID = 7 };
+// epilogue numbering: vj_common.h (shared with vj_gemm256.hip and the public header)
 
 struct GemmArgs {
   const bf16_t* A;

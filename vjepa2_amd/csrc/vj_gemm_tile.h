@@ -20,10 +20,8 @@ namespace {
 #define VJ_GEMM_DMA_WAVES 4
 #endif
 
-// EPI_BF16_RESID: bf16 residual in (aux), bf16 out — the no-grad target encoder's residual stream in
-// the reference's own autocast precision (x = x + proj(...) in bf16), half the epilogue bytes of F32_RESID
-enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5, EPI_PARTIAL = 6,
-       EPI_BF16_RESID = 7 };
+// epilogue numbering: vj_common.h (EPI_BF16_RESID: the no-grad target encoder's residual stream in the
+// reference's own autocast precision, x = x + proj(...) in bf16, half the epilogue bytes of F32_RESID)
 
 using RopeP = VjRope;
 

@@ -680,12 +680,15 @@ __global__ void k_fill_rows(int R, int D, float* __restrict__ dst, long ldd, con
   for (int i = threadIdx.x; i < D; i += blockDim.x) d[i] = vec[i];
 }
 
-// dst[r] += table[idx[r]]   (sincos positional embeddings, non-RoPE variant)
+// dst[r] += table[idx[r]]   (sincos positional embeddings, non-RoPE variant). Ids outside [0, trows)
+// are never read (the row is left as is): a bad device index cannot fault; host callers validate
+// CPU indices and raise as the reference's gather would.
 __global__ void k_add_rows(int R, int D, float* __restrict__ dst, long ldd, const float* __restrict__ table,
-                           long ldt, const int* __restrict__ idx, int idx_mod) {
+                           long ldt, int trows, const int* __restrict__ idx, int idx_mod) {
   const int r = blockIdx.x;
   if (r >= R) return;
   const long t = idx ? idx[r] : (r % idx_mod);
+  if (t < 0 || t >= trows) return;
   for (int i = threadIdx.x; i < D; i += blockDim.x) dst[(long)r * ldd + i] += table[t * ldt + i];
 }
 
@@ -1244,11 +1247,14 @@ extern "C" int vj_fill_rows(int R, int D, float* dst, long ldd, const int* idx, 
   return VJ_OK;
 }
 
-extern "C" int vj_add_rows(int R, int D, float* dst, long ldd, const float* table, long ldt, const int* idx,
-                           int idx_mod, void* stream) {
+extern "C" int vj_add_rows(int R, int D, float* dst, long ldd, const float* table, long ldt, int trows,
+                           const int* idx, int idx_mod, void* stream) {
   if (R == 0) return VJ_OK;
   VJ_CHECK_ARG(idx || idx_mod > 0, "vj_add_rows: idx or idx_mod");
-  hipLaunchKernelGGL(k_add_rows, dim3(R), dim3(128), 0, (hipStream_t)stream, R, D, dst, ldd, table, ldt, idx, idx_mod);
+  VJ_CHECK_ARG(trows > 0 && (idx || idx_mod <= trows), "vj_add_rows: idx_mod %d exceeds the table's %d rows", idx_mod,
+               trows);
+  hipLaunchKernelGGL(k_add_rows, dim3(R), dim3(128), 0, (hipStream_t)stream, R, D, dst, ldd, table, ldt, trows, idx,
+                     idx_mod);
   VJ_LAUNCH_CHECK("vj_add_rows");
   return VJ_OK;
 }

@@ -59,12 +59,14 @@ class ClipAggregation(nn.Module):
             if self.pos_embed is not None and clip_indices is not None:
                 # row (b, c, t, s) += pos_embed[clip_indices[c][b, t * tubelet]] (apply_masks of the table)
                 idx = torch.stack([ci[:, ::self.tubelet_size] for ci in clip_indices], 1)  # [B, clips, T]
-                # vj_add_rows does not bounds-check its row ids: raise on the host as the reference's
-                # gather would (an index past the sincos table)
-                lo, hi = int(idx.min()), int(idx.max())
-                if lo < 0 or hi >= self.pos_embed.shape[1]:
-                    raise IndexError(f"clip index {hi if hi >= self.pos_embed.shape[1] else lo} out of range for "
-                                     f"the temporal pos_embed of {self.pos_embed.shape[1]} frames")
+                # CPU indices (the eval loaders' clip_indices) are validated here and raise as the
+                # reference's gather would; device indices are not read back (no host sync per forward):
+                # vj_add_rows never reads a table row outside [0, rows) and leaves such a row unchanged
+                if not idx.is_cuda:
+                    lo, hi = int(idx.min()), int(idx.max())
+                    if lo < 0 or hi >= self.pos_embed.shape[1]:
+                        raise IndexError(f"clip index {hi if hi >= self.pos_embed.shape[1] else lo} out of range "
+                                         f"for the temporal pos_embed of {self.pos_embed.shape[1]} frames")
                 idx = idx.to(device=o.device, dtype=torch.int32)
                 idx = idx.reshape(B, num_clips * T, 1).expand(B, num_clips * T, S).reshape(-1).contiguous()
                 table = self.pos_embed[0].detach().float().contiguous()

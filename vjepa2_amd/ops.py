@@ -532,7 +532,7 @@ def fill_rows(dst, idx, vec):
 def add_rows(dst, table, idx=None, idx_mod=0):
     _dev(dst, table, idx)
     _call("vj_add_rows", dst.shape[0], dst.shape[1], _p(dst), _rowmajor(dst, "dst"), _p(table),
-         _rowmajor(table, "table"), _p(idx), int(idx_mod), _stream())
+         _rowmajor(table, "table"), table.shape[0], _p(idx), int(idx_mod), _stream())
 
 
 def pred_index(mx, my, row0, N, pos, ctx_dst, tgt_rows, loss_rows=None):

@@ -423,24 +423,20 @@ def test_fused_rope_paths(M, hd, H, monkeypatch):
     w = (0.1 * torch.randn(3 * D, K, generator=g)).to(DEV).bfloat16()
     b = torch.randn(3 * D, generator=g).to(DEV)
     fused = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
-    if M >= 1024:  # ping-pong kernel == one-tile-per-workgroup kernel, bitwise
-        prev = os.environ.get("VJ_GEMM_PP")
-        for pp in ("1", "0"):
-            monkeypatch.setenv("VJ_GEMM_PP", pp)
-            other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
-            assert torch.equal(fused, other), f"qkv_rope: VJ_GEMM_PP={pp} differs from the default kernel"
+    if M >= 1024:
+        monkeypatch.setenv("VJ_GEMM_MF", "16")
+        f16 = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
         for bm in ("1", "0"):  # 192-row tiles (where N takes 256-wide ones) == 256-row tiles, bitwise
             monkeypatch.setenv("VJ_GEMM_BM192", bm)
             other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
-            assert torch.equal(fused, other), f"qkv_rope: VJ_GEMM_BM192={bm} differs from the default kernel"
+            assert torch.equal(f16, other), f"qkv_rope: VJ_GEMM_BM192={bm} differs from the 16x16x32 kernel"
         monkeypatch.delenv("VJ_GEMM_BM192")
-        monkeypatch.setenv("VJ_GEMM_PP", "2")  # 32x32x16 form: other K order, one bf16 rounding apart
-        other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
-        _close(other, fused, 1e-3, 8e-3, "qkv_rope VJ_GEMM_PP=2 vs default")
-        if prev is None:
-            monkeypatch.delenv("VJ_GEMM_PP")
-        else:
-            monkeypatch.setenv("VJ_GEMM_PP", prev)
+        # 32x32x16 form (256-wide tiles only): another K order inside each MFMA, one bf16 rounding apart
+        monkeypatch.setenv("VJ_GEMM_MF", "32")
+        f32x = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
+        monkeypatch.delenv("VJ_GEMM_MF")
+        _close(f32x, f16, 1e-3, 8e-3, "qkv_rope 32x32x16 vs 16x16x32")
+        assert torch.equal(fused, f16) or torch.equal(fused, f32x), "default kernel is neither MFMA form"
     # expected: our own f32 GEMM (same accumulation), RoPE in fp32 by the oracle
     y32 = ops.linear_fwd(x, w, b, ops.EPI_F32).cpu()
     idl = ids.cpu().long()[None]
@@ -668,19 +664,20 @@ def test_adamw_ema_fused_equals_separate(skip):
 
 @pytest.mark.parametrize("K", [64, 192, 256, 1024])
 @pytest.mark.parametrize("pxcd", [None, "1", "3"])
-def test_gemm_pingpong_matches_one_tile_kernel(K, pxcd, monkeypatch):
-    """The ping-pong kernel (vj_gemm_pp.hip: two wave groups alternating K-loop / epilogue over one
-    LDS ring) against the one-tile-per-workgroup kernel (VJ_GEMM_PP=0) on every epilogue: the same
-    per-wave tile and K order, so the outputs are BITWISE equal; and against fp32 math. K = 64 / 128
-    make one / two K-tiles per tile (the group hand-over DMAs span tiles); VJ_GEMM_PXCD = 1 / 3 puts
-    many tiles on each block (many periods, odd and even counts) and N = 200 a ragged last column.
-    K = 64 / 128 (fewer K-tiles than the ring's 3 stages) take the one-tile kernel: trivially equal."""
+def test_gemm_mfma32_matches_mfma16(K, pxcd, monkeypatch):
+    """The 32x32x16 form of the 256 x 256-tile kernel (VJ_GEMM_MF=32: waves 4 x 2, wave tile 64 x 128,
+    B staged with a 32-row permutation) against the 16x16x32 form (VJ_GEMM_MF=16) on every epilogue:
+    another K summation order inside each MFMA, so f32 outputs agree to accumulation rounding and bf16
+    outputs to one rounding step (few of them differ at all); both against fp32 math. K = 64 / 192 /
+    256 make 1 / 3 / 4 K-tiles (tail paths), VJ_GEMM_PXCD = 1 / 3 many tiles per block (the next
+    tile's stages DMA'd under the epilogue), M = 2100 / 1333 ragged last row tiles and N = 1000 a
+    ragged last column tile."""
     from vjepa2_amd import ops
 
     if pxcd:
         monkeypatch.setenv("VJ_GEMM_PXCD", pxcd)
     g = torch.Generator(device="cpu").manual_seed(K)
-    for M, N in [(2100, 384), (1333, 200)]:
+    for M, N in [(2100, 512), (1333, 1000)]:
         X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
         W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
         b = torch.randn(N, generator=g).to(DEV)
@@ -702,32 +699,25 @@ def test_gemm_pingpong_matches_one_tile_kernel(K, pxcd, monkeypatch):
             torch.cuda.synchronize()
             return {k: v.detach().clone() for k, v in outs.items()}
 
-        monkeypatch.setenv("VJ_GEMM_PP", "1")
-        pp = run()
-        monkeypatch.setenv("VJ_GEMM_PP", "0")
-        one = run()
-        monkeypatch.delenv("VJ_GEMM_PP")
-        for k in pp:
-            assert torch.equal(pp[k], one[k]), f"ping-pong != one-tile kernel: {k} M={M} N={N} K={K} pxcd={pxcd}"
-        _close(pp["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "pp EPI_F32")
-        _close(pp["f32_resid"], ref + resid, 1e-4 * math.sqrt(K) * 4, 1e-4, "pp EPI_F32_RESID")
-        _close(pp["bf16"], ref, 1e-3, 8e-3, "pp EPI_BF16")
-        assert torch.equal(pp["gelu_a"], pp["gelu_nosave"])
-        _close(pp["gelu_bwd"], (X.float() @ W.float().t()) * dgs.float(), 2e-3, 1.5e-2, "pp EPI_GELU_BWD")
-        # the 32x32x16 form (VJ_GEMM_PP=2): another K summation order inside each MFMA, so f32 outputs
-        # agree with the one-tile kernel to accumulation rounding and bf16 outputs to one rounding step
-        monkeypatch.setenv("VJ_GEMM_PP", "2")
-        p32 = run()
-        monkeypatch.delenv("VJ_GEMM_PP")
+        monkeypatch.setenv("VJ_GEMM_BM192", "0")  # 256-row tiles for both forms
+        monkeypatch.setenv("VJ_GEMM_MF", "16")
+        m16 = run()
+        monkeypatch.setenv("VJ_GEMM_MF", "32")
+        m32 = run()
+        monkeypatch.delenv("VJ_GEMM_MF")
+        monkeypatch.delenv("VJ_GEMM_BM192")
         tol32 = 2e-6 * math.sqrt(K) * float(ref.abs().max())
         for k in ("f32", "f32_resid"):
-            _close(p32[k], one[k], tol32, 1e-5, f"pp32 {k} vs one-tile")
+            _close(m32[k], m16[k], tol32, 1e-5, f"mfma32 {k} vs mfma16 (M={M} N={N} K={K})")
         for k in ("bf16", "bf16_resid", "gelu_a", "gelu_d", "gelu_bwd"):
-            _close(p32[k], one[k], 1e-3, 8e-3, f"pp32 {k} vs one-tile")
-            frac = (p32[k] != one[k]).float().mean().item()
-            assert frac < 0.05, f"pp32 {k}: {frac:.3f} of the bf16 outputs differ from the one-tile kernel"
-        assert torch.equal(p32["gelu_a"], p32["gelu_nosave"])
-        _close(p32["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "pp32 EPI_F32 vs fp32")
+            _close(m32[k], m16[k], 1e-3, 8e-3, f"mfma32 {k} vs mfma16 (M={M} N={N} K={K})")
+            frac = (m32[k] != m16[k]).float().mean().item()
+            assert frac < 0.05, f"mfma32 {k}: {frac:.3f} of the bf16 outputs differ from the 16x16x32 form"
+        assert torch.equal(m32["gelu_a"], m32["gelu_nosave"])
+        _close(m32["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "mfma32 EPI_F32 vs fp32")
+        _close(m32["f32_resid"], ref + resid, 1e-4 * math.sqrt(K) * 4, 1e-4, "mfma32 EPI_F32_RESID vs fp32")
+        _close(m32["bf16"], ref, 1e-3, 8e-3, "mfma32 EPI_BF16 vs fp32")
+        _close(m32["gelu_bwd"], (X.float() @ W.float().t()) * dgs.float(), 2e-3, 1.5e-2, "mfma32 EPI_GELU_BWD")
 
 
 @pytest.mark.parametrize("K", [64, 128, 1024])

@@ -1,5 +1,10 @@
-// Large-tile bf16 GEMM for gfx950: 256 x BN x 64 tiles (BN = 256 or 128), 512 threads = 8 waves
-// (2 in M x 4 in N), one workgroup per CU (LDS 144 / 112 KB), v_mfma_f32_16x16x32_bf16.
+// Large-tile bf16 GEMM for gfx950: 256 x BN x 64 tiles (BN = 256 or 128), 512 threads = 8 waves,
+// one workgroup per CU (LDS 144 / 112 KB). Two MFMA forms of the same tile:
+//   M32 = false: v_mfma_f32_16x16x32_bf16, waves 2 (M) x 4 (N), wave tile 128 x 64;
+//   M32 = true : v_mfma_f32_32x32x16_bf16, waves 4 (M) x 2 (N), wave tile 64 x 128 (K-major A and B,
+//                256-wide tiles): each MFMA holds its SIMD's vector-issue port 8 of 32 cycles instead of
+//                8 of 16, so the LDS-DMA issue, fragment reads and barrier of the main loop get 3x
+//                the free issue slots per flop; the same 24 ds_read_b128 per wave and K-tile.
 // Same operand/epilogue contract as vj_gemm.hip (K-major or MN-major A and B, fused epilogues);
 // used for the forward and data-gradient GEMMs of the encoder / predictor blocks (M = tokens) and the
 // split-K weight gradients.
@@ -21,34 +26,22 @@
 #include <type_traits>
 #include "vj_gemm_tile.h"
 
-// 8-wave main loop: the next K-tile's DMA pieces issued between the last phase's MFMAs instead of in
-// one burst after the barrier (1: B pieces halfway; 2: A pieces after the first quarter as well).
-// Measured (tools/bench_kernels.py, profiles/r03_gemm_spread_kernels.txt): 1 = -2..-7 % on the
-// ViT-L forward / data-gradient shapes; the B pieces after 3 of the phase's 4 m-tiles (SPLIT_AT 3)
-// a further 0..-5 % (r03_gemm_split_kernels.txt); spreading the 2W kernel's pieces did not pay.
-#ifndef VJ_GEMM_SPREAD
-#define VJ_GEMM_SPREAD 1
-#endif
-#ifndef VJ_GEMM_SPREAD32
-#define VJ_GEMM_SPREAD32 0
-#endif
-#ifndef VJ_GEMM_SPLIT_AT
-#define VJ_GEMM_SPLIT_AT 3
-#endif
-// VJ_GEMM_DMA8_S1 = 1: the RoPE / GELU / GELU-backward tiles also take the waves-0-3 DMA in their main
-// loop (the next tile's stage 1, issued around the epilogue, always goes out from all 8 waves)
-#ifndef VJ_GEMM_DMA8_S1
-#define VJ_GEMM_DMA8_S1 0
-#endif
-#ifndef VJ_GEMM_DMA_SPLIT  // 1: with 4 DMA waves, A pieces from waves 0-3 and B pieces from waves 4-7
-#define VJ_GEMM_DMA_SPLIT 0
-#endif
-#ifndef VJ_GEMM_DMA_HI  // 1: the 4 DMA-issuing waves are 4-7
-#define VJ_GEMM_DMA_HI 0
-#endif
-#ifndef VJ_GEMM_S1_ALL  // 0: the next tile's stage 1 from the DMA-issuing waves only (as the main loop)
-#define VJ_GEMM_S1_ALL 1
-#endif
+// Schedule choices fixed by round-3 measurements (the variants were removed from the source; the
+// numbers are in DESIGN.md and profiles/r03_gemm_*):
+//  * 8-wave main loop: only the A pieces of K-tile t + 2 go out after the barrier; the B pieces are
+//    issued after 3 of the last phase's 4 m-tiles (SPLIT_AT; 16x16x32 form) or 6 of its 8 MFMAs
+//    (32x32x16 form): -2..-7 % and a further 0..-5 % on the ViT-L shapes (r03_gemm_spread_kernels.txt,
+//    r03_gemm_split_kernels.txt). Also the A pieces after the first m-tile: slower.
+//  * on 256-wide bf16 tiles without a VALU-heavy epilogue only waves 0-3 issue the main-loop LDS-DMA
+//    (DMA_WAVES; their SIMD partners keep issuing MFMAs); the next tile's stage 1, issued around the
+//    epilogue, goes out from all 8 waves (r03_gemm_dmaw4_kernels.txt, r03_gemm_s1all_step_ab.txt).
+//    Slower and removed: the RoPE / GELU tiles on 4 DMA waves, A / B pieces split over waves 0-3 /
+//    4-7, the DMA from waves 4-7, s_setprio around the MFMA clusters or for waves 4-7.
+//  * one m-tile of residual / saved-derivative rows prefetched ahead in the direct epilogue (deeper:
+//    no faster, r03 stamps).
+constexpr int SPLIT_AT = 3;
+constexpr int DMA_WAVES = 4;
+constexpr int AUX_PF = 1;
 
 namespace {
 
@@ -63,28 +56,33 @@ __device__ long vj_gemm_stamps[2048 * 16 * 4];
 // BMT = 192 (8-wave, K-major bf16, 256-wide direct-store tiles only): 96-row wave tiles (3 m-tiles
 // per M-half) for problems whose 256-row tile count leaves a round of CUs under-filled (context
 // GEMMs, M ~ 11.7k: 184 tiles of 256 x 256 on 256 CUs -> 244 tiles of 192 x 256).
-template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256>
+template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, bool M32 = false>
 __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   static_assert(!F8 || (AK && BKM && EPI != EPI_PARTIAL && EPI != EPI_GELU_BWD), "fp8: forward GEMMs only");
   static_assert(NWV == 8 || (NWV == 4 && AK && BKM && !F8), "2-workgroup GEMM: K-major bf16 operands only");
+  static_assert(!M32 || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256),
+                "32x32x16 form: 8-wave K-major bf16 256 x 256 tiles");
   constexpr int BM = BMT;
-  constexpr int MH = BM / 64;     // m-tiles per M-half of a wave (4 / 3)
-  constexpr int WM = BM / 2;      // wave tile rows (128 / 96)
+  constexpr int MH = BM / 64;     // virtual 16-row m-tiles per half of the wave's rows (4 / 3)
   constexpr int BK = NWV == 8 ? 64 : 32;
   constexpr int NT = NWV * 64;
-  constexpr int WNX = NWV / 2;    // waves across N (4 / 2); 2 waves across M
+  constexpr int WNX = M32 ? 2 : NWV / 2;  // waves across N (16x16x32: 4 / 2, 32x32x16: 2)
+  constexpr int WMX = NWV / WNX;          // waves across M (2 / 4)
+  constexpr int WM = BM / WMX;            // wave tile rows (128 / 96; 32x32x16: 64)
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int WN = BN / WNX;    // wave tile columns (64 / 32)
-  constexpr int NTN = WN / 16;    // 16-wide n tiles per wave (4 / 2)
-  // LDS-DMA issuers: VJ_GEMM_DMA_WAVES = 4 -> waves 0-3 only on 256-wide tiles (their SIMD partners
-  // 4-7 keep issuing MFMAs meanwhile), except the RoPE / GELU / GELU-backward tiles, whose next-tile
-  // stage 1 goes out right before (or in) their VALU-heavy epilogue, where waves 0-3 would start it
-  // 16 pieces late; 128-wide tiles (the predictor's N = 384) measured slower with it. 8 = all waves.
+  constexpr int WN = BN / WNX;    // wave tile columns (64 / 32; 32x32x16: 128)
+  constexpr int PB = M32 ? 32 : 16;  // MFMA output block width
+  constexpr int NTN = WN / PB;    // n blocks per wave (4 / 2)
+  constexpr int MB32 = WM / 32;   // 32x32x16: m blocks per wave (2)
+  // LDS-DMA issuers: DMA_WAVES = 4 -> waves 0-3 only on 256-wide tiles (their SIMD partners 4-7 keep
+  // issuing MFMAs meanwhile), except the RoPE / GELU / GELU-backward tiles, whose next-tile stage 1
+  // goes out right before (or in) their VALU-heavy epilogue, where waves 0-3 would start it 16
+  // pieces late; 128-wide tiles (the predictor's N = 384) measured slower with it.
   constexpr bool VALU_EPI = EPI == EPI_ROPE || EPI == EPI_GELU || EPI == EPI_GELU_BWD;
-  constexpr int DMAW = NWV != 8 ? NWV : (VJ_GEMM_DMA_WAVES == 8 || (VALU_EPI && !VJ_GEMM_DMA8_S1) || BN != 256 || F8) ? 8 : VJ_GEMM_DMA_WAVES;
-  // K-major B with 4 n-tiles per wave: permuted B staging + stores straight from registers (16-B
+  constexpr int DMAW = NWV != 8 ? NWV : (VALU_EPI || BN != 256 || F8) ? 8 : DMA_WAVES;
+  // K-major B with 4 n blocks per wave: permuted B staging + stores straight from registers (16-B
   // f32 / 8-B bf16 per row); 128-wide tiles would store 4-8 B per lane, so they keep the LDS path
   constexpr bool DIRECT = BKM && NTN == 4;
   static_assert(BMT == 256 || (BMT == 192 && NWV == 8 && !F8 && AK && DIRECT), "192-row tiles: 8-wave direct K-major bf16");
@@ -116,11 +114,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   const int run0 = xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q;
   const int runend = run0 + q + (xcd < rmd ? 1 : 0);
   if (run0 + jb >= runend) return;
-  // stagger: the 8-wave kernel delays odd blocks of an XCD; the two-workgroup kernel delays the
-  // second workgroup of each CU (blocks jb and jb + P/2 of an XCD share a CU), so the two
-  // workgroups' epilogues fall under each other's main loops
-  if (g.stagger > 0 && (NWV == 4 ? jb >= (P >> 1) : (jb & 1)))
-    for (int i = 0; i < g.stagger; ++i) __builtin_amdgcn_s_sleep(32);
 
   auto make_tile = [&](int wg) {
     Tile T;
@@ -159,28 +152,23 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     return make_rsrc(bbase, BKM ? clampb((long)(g.N - T.n0) * g.ldb * 2 - kb * 2L)
                                 : clampb(((long)(g.K - kb) * g.ldb - T.n0) * 2));
   };
-  // DSPLIT (VJ_GEMM_DMA_SPLIT, with 4 DMA waves): A pieces from waves 0-3, B pieces from waves 4-7
-  constexpr bool DSPLIT = VJ_GEMM_DMA_SPLIT && NWV == 8 && DMAW == 4;
-  // VJ_GEMM_DMA_HI: the 4 DMA waves are 4-7 (the younger half) instead of 0-3
-  const int dwv = (VJ_GEMM_DMA_HI && NWV == 8 && DMAW == 4 && !DSPLIT) ? wave - 4 : wave;
-  const bool a_iss = DMAW == 8 || (dwv >= 0 && dwv < DMAW);
-  const bool b_iss = DSPLIT ? wave >= 4 : a_iss;
-  const int bwv = DSPLIT ? wave - 4 : dwv;
+  const bool iss = DMAW == 8 || wave < DMAW;  // this wave issues main-loop LDS-DMA pieces
   auto load_k = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, const Tile& T, int t, int slot,
                     int lane) {
     LDS_AS char* s = smem + slot * STAGE;
-    if (a_iss) stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, dwv, lane);
-    if (b_iss) stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, bwv, lane);
+    if (iss) {
+      stage<AK, BM, false, DMAW, BK, WNX, PB>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
+      stage<BKM, BN, DIRECT, DMAW, BK, WNX, PB>(rb, g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, wave, lane);
+    }
   };
   auto load_tile = [&](const Tile& T, int t, int slot, int lane) {
     load_k(rsrc_a(T), rsrc_b(T), T, t, slot, lane);
   };
   // the next tile's stage 1, issued around the epilogue (no MFMAs to keep fed): all 8 waves
   auto load_tile8 = [&](const Tile& T, int t, int slot, int lane) {
-    if (!VJ_GEMM_S1_ALL) return load_tile(T, t, slot, lane);
     LDS_AS char* s = smem + slot * STAGE;
-    stage<AK, BM, false, NWV, BK, WNX>(rsrc_a(T), g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
-    stage<BKM, BN, DIRECT, NWV, BK, WNX>(rsrc_b(T), g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, wave, lane);
+    stage<AK, BM, false, NWV, BK, WNX, PB>(rsrc_a(T), g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
+    stage<BKM, BN, DIRECT, NWV, BK, WNX, PB>(rsrc_b(T), g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, wave, lane);
   };
 
   // per-kernel tables (RoPE): global loads issued before the first DMA (so their waits do not queue
@@ -211,11 +199,22 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       if (e < ntab) rtab[e] = rpf[i];
     }
   }
-#if VJ_GEMM_SPRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
-#endif
 
-  f32x4 acc[2 * MH][NTN];
+  // Accumulators. 16x16x32: acc[i][j] = m-tile i (16 rows), n block j. 32x32x16: acc32[mb][j] = m block
+  // mb (32 rows), n block j. The epilogue walks 2 * MH "virtual m-tiles" of 4 rows per lane either way:
+  // ACC(i, j, r) is lane's value of row r of virtual m-tile i in n block j, ROWOFF(i) that tile's
+  // first row within the wave tile (the lane's 4-row offset comes on top: 4 (lane >> 4) or 4 (lane >> 5)).
+  [[maybe_unused]] f32x4 acc[M32 ? 1 : 2 * MH][NTN];
+  [[maybe_unused]] f32x16 acc32[M32 ? MB32 : 1][NTN];
+  auto accv = [&](int i, int j, int r) -> float {
+    if constexpr (M32) return acc32[i >> 2][j][4 * (i & 3) + r];
+    else return acc[i][j][r];
+  };
+  auto accs = [&](int i, int j, int r, float v) {
+    if constexpr (M32) acc32[i >> 2][j][4 * (i & 3) + r] = v;
+    else acc[i][j][r] = v;
+  };
+  auto rowoff = [](int i) { return M32 ? (i >> 2) * 32 + 8 * (i & 3) : i * 16; };
   bf16x8 Aa[MH], Ab[MH], Ba[NTN], Bb[NTN];
   // A fragments of M-half mh (4 m-tiles), k-step ks; B fragments of all NTN n-tiles, k-step ks
   auto rdA = [&](bf16x8 (&X)[MH], int slot, int mh, int ks) {
@@ -227,6 +226,27 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     const LDS_AS char* s = smem + slot * STAGE + A_BYTES;
 #pragma unroll
     for (int j = 0; j < NTN; ++j) Y[j] = frag<BKM, BN, BK>(s, wc * WN + j * 16, ks, lane);
+  };
+  // ---- 32x32x16 (M32) fragments of k-step ks (16 deep): lane l reads row (l & 31) of a 32-row block,
+  // 16-B chunk 2 ks + (l >> 5); the K-major swizzle (chunk ^= (row >> 1) & 7) keeps every 16-lane
+  // quarter of a ds_read_b128 on 16 distinct bank slots. A: the wave's MB32 m blocks (into X[0..]),
+  // B: its NTN n blocks (LDS rows wc * 128 + 32 j, permuted at staging: PB = 32).
+  auto rd32 = [&](bf16x8 (&X)[MH], bf16x8 (&Y)[NTN], int slot, int ks) {
+    const LDS_AS char* s = smem + slot * STAGE;
+    const int lr = lane & 31;
+    const int off = lr * 128 + (((2 * ks + (lane >> 5)) ^ ((lr >> 1) & 7)) * 16);
+#pragma unroll
+    for (int i = 0; i < MB32; ++i) X[i] = *(const LDS_AS bf16x8*)(s + (wr * WM + 32 * i) * 128 + off);
+#pragma unroll
+    for (int j = 0; j < NTN; ++j) Y[j] = *(const LDS_AS bf16x8*)(s + A_BYTES + (wc * WN + 32 * j) * 128 + off);
+  };
+  // MFMAs q0 .. q1 - 1 of a k-step (q = mb * NTN + j)
+  auto mm32 = [&](const bf16x8 (&X)[MH], const bf16x8 (&Y)[NTN], int q0, int q1) {
+#pragma unroll
+    for (int q = 0; q < MB32 * NTN; ++q)
+      if (q >= q0 && q < q1)
+        acc32[q / NTN][q % NTN] =
+            __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[q / NTN], Y[q % NTN], acc32[q / NTN][q % NTN], 0, 0, 0);
   };
   // ---- fp8 (F8): one K-tile row is 128 B = 128 e4m3 values = ONE v_mfma_scale_f32_16x16x128_f8f6f4
   // per 16x16 output tile. Its 32-B lane operand is the two 16-B fragments the bf16 path reads for
@@ -264,19 +284,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
                                                                               0, f8sa[2 * qq + i], 0, f8sb[j]);
   };
   auto mm = [&](const bf16x8 (&X)[MH], int mh, const bf16x8 (&Y)[NTN]) {
-#if VJ_GEMM_PRIO
-    __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
     for (int i = 0; i < MH; ++i)
 #pragma unroll
       for (int j = 0; j < NTN; ++j)
         acc[mh * MH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * MH + i][j], 0, 0, 0);
-#if VJ_GEMM_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
   };
-  // m-tiles i0 .. i1 - 1 of one phase (SPREAD splits the last phase around the B DMA pieces)
+  // m-tiles i0 .. i1 - 1 of one phase (the last phase is split around the B DMA pieces)
   auto mm_rows = [&](const bf16x8 (&X)[MH], int mh, const bf16x8 (&Y)[NTN], int i0, int i1) {
 #pragma unroll
     for (int i = 0; i < MH; ++i)
@@ -314,10 +328,17 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       const int t = threadIdx.x;
       if (t < BM && cur.m0 + t < g.M) pf_id = g.rope.ids ? g.rope.ids[cur.m0 + t] : (cur.m0 + t) % g.rope.mod;
     }
+    if constexpr (M32) {
 #pragma unroll
-    for (int i = 0; i < 2 * MH; ++i)
+      for (int i = 0; i < MB32; ++i)
 #pragma unroll
-      for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NTN; ++j) acc32[i][j] = f32x16{};
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2 * MH; ++i)
+#pragma unroll
+        for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     if constexpr (F8) {  // this tile's per-row scale exponents (retired by the wait below)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -340,17 +361,24 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     if constexpr (F8) {
       rdA8(Xa, par, 0);
       rdB8(0, NTN / 2, par);
+    } else if constexpr (M32) {
+      rd32(Aa, Ba, par, 0);
     } else {
       rdA(Aa, par, 0, 0);
       rdB(Ba, par, 0);
     }
 
-    // Per K-tile t: 4 phases (k-step, M-half) = (0,0) (0,1) (1,0) (1,1), 4*NTN MFMAs each; the
-    // fragments of the NEXT phase are read while the current phase's MFMAs run. One barrier per
-    // tile, before phase 3 (whose prefetch reads tile t+1): it retires this wave's DMA of tile t+1
-    // (issued one tile earlier) and its reads of tile t; then slot (t + par) & 1 is free for the
-    // DMA of tile t+2, or of the next tile's stages once this tile has none left.
+    // Per K-tile t: 4 phases, each with the fragments of the NEXT phase read while the current
+    // phase's MFMAs run: 16x16x32 (k-step, M-half) = (0,0) (0,1) (1,0) (1,1), 4*NTN MFMAs each;
+    // 32x32x16 k-steps 0..3, 8 MFMAs each. One barrier per tile, before phase 3 (whose prefetch reads
+    // tile t+1): it retires this wave's DMA of tile t+1 (issued one tile earlier) and its reads of
+    // tile t; then slot (t + par) & 1 is free for the DMA of tile t+2, or of the next tile's stages
+    // once this tile has none left.
     const __amdgpu_buffer_rsrc_t ra = rsrc_a(cur), rb = rsrc_b(cur);
+    // 8-wave bf16 main loop: only the A pieces of K-tile t + 2 go out after the barrier; the B pieces
+    // are issued inside the last phase's MFMAs (SPLIT: m-tiles / MFMAs before them)
+    constexpr bool SPREAD = NWV == 8 && !F8 && BK == 64;
+    constexpr int SPLIT = M32 ? 6 : (MH == 4 ? SPLIT_AT : MH - 1);
     // one K-tile; TAIL (the last two K-tiles) DMAs the next tile's stages instead of this tile's
     auto ktile = [&](const int t, auto tail_c) {
       constexpr bool TAIL = decltype(tail_c)::value;
@@ -372,6 +400,20 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         __builtin_amdgcn_sched_barrier(0);
         mm8(Xa, 2, 0, NTN);
         __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (M32) {
+        // k-steps 0..2 (fragments alternate between (Aa, Ba) and (Ab, Bb))
+        rd32(Ab, Bb, sl, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm32(Aa, Ba, 0, 8);
+        __builtin_amdgcn_sched_barrier(0);
+        rd32(Aa, Ba, sl, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mm32(Ab, Bb, 0, 8);
+        __builtin_amdgcn_sched_barrier(0);
+        rd32(Ab, Bb, sl, 3);
+        __builtin_amdgcn_sched_barrier(0);
+        mm32(Aa, Ba, 0, 8);
+        __builtin_amdgcn_sched_barrier(0);
       } else if constexpr (BK == 32) {
         // one k-step: phase 0 = (M-half 0) under the read of M-half 1's A fragments; phase 1 after
         // the barrier, the next K-tile's fragments read under its MFMAs
@@ -380,22 +422,22 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         mm(Aa, 0, Ba);
         __builtin_amdgcn_sched_barrier(0);
       } else {
-      release(Aa, Ba);
-      rdA(Ab, sl, 1, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(Aa, 0, Ba);
-      __builtin_amdgcn_sched_barrier(0);
-      release(Ab, Ba);
-      rdA(Aa, sl, 0, 1);
-      rdB(Bb, sl, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(Ab, 1, Ba);
-      __builtin_amdgcn_sched_barrier(0);
-      release(Aa, Bb);
-      rdA(Ab, sl, 1, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(Aa, 0, Bb);
-      __builtin_amdgcn_sched_barrier(0);
+        release(Aa, Ba);
+        rdA(Ab, sl, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(Aa, 0, Ba);
+        __builtin_amdgcn_sched_barrier(0);
+        release(Ab, Ba);
+        rdA(Aa, sl, 0, 1);
+        rdB(Bb, sl, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(Ab, 1, Ba);
+        __builtin_amdgcn_sched_barrier(0);
+        release(Aa, Bb);
+        rdA(Ab, sl, 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(Aa, 0, Bb);
+        __builtin_amdgcn_sched_barrier(0);
       }
       if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next tile's stage 0 stays in flight
@@ -405,18 +447,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       }
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      // SPREAD (8-wave, bf16, main loop): only the A pieces of K-tile t + 2 go out here; the B pieces
-      // are issued between the two halves of the last phase's MFMAs, so the post-barrier DMA burst of
-      // both waves of a SIMD is half as long
-      constexpr bool SPREAD = VJ_GEMM_SPREAD && NWV == 8 && !F8 && BK == 64;
-      // the same for the two-workgroup kernel's 32-deep K-tiles (one phase after the barrier)
-      constexpr bool SPREAD32 = VJ_GEMM_SPREAD32 && NWV == 4 && BK == 32;
-      constexpr int SPLIT_AT = MH == 4 ? VJ_GEMM_SPLIT_AT : MH - 1;  // m-tiles of the last phase before the B pieces
       if constexpr (!TAIL) {
-        if constexpr (SPREAD || SPREAD32) {
-          if ((SPREAD32 || VJ_GEMM_SPREAD == 1) && a_iss)
-            stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff, smem + sl * STAGE,
-                                                 dwv, lane);
+        if constexpr (SPREAD) {
+          if (iss)
+            stage<AK, BM, false, DMAW, BK, WNX, PB>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff,
+                                                     smem + sl * STAGE, wave, lane);
         } else {
           load_k(ra, rb, cur, t + 2, sl, lane);
         }
@@ -433,6 +468,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           if (EARLY1 && nx.nk > 1) load_tile8(nx, 1, sl, lt);
         }
       }
+      auto b_pieces = [&] {
+        if (iss)
+          stage<BKM, BN, DIRECT, DMAW, BK, WNX, PB>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
+                                                     smem + sl * STAGE + A_BYTES, wave, lane);
+      };
       if constexpr (F8) {
         // q3; the next K-tile's q0 A fragments and lower B n-tiles are read under it
         if (t + 1 < nk) rdA8(Xa, sl ^ 1, 0);
@@ -443,18 +483,22 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         __builtin_amdgcn_sched_barrier(0);
         mm8(Xb, 3, NTN / 2, NTN);
         __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (BK == 32) {
-        if constexpr (SPREAD32 && !TAIL) {
-          mm_rows(Ab, 1, Ba, 0, 2);
+      } else if constexpr (M32) {
+        // k-step 3; the next K-tile's k-step 0 fragments are read under it
+        if (t + 1 < nk) rd32(Aa, Ba, sl ^ 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (SPREAD && !TAIL) {
+          mm32(Ab, Bb, 0, SPLIT);
           __builtin_amdgcn_sched_barrier(0);
-          if (DMAW == 8 || wave < DMAW)
-            stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
-                                                   smem + sl * STAGE + A_BYTES, wave, lane);
+          b_pieces();
           __builtin_amdgcn_sched_barrier(0);
-          mm_rows(Ab, 1, Ba, 2, 4);
+          mm32(Ab, Bb, SPLIT, 8);
         } else {
-          mm(Ab, 1, Ba);
+          mm32(Ab, Bb, 0, 8);
         }
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (BK == 32) {
+        mm(Ab, 1, Ba);
         __builtin_amdgcn_sched_barrier(0);
         if (t + 1 < nk) {  // overwrite Aa / Ba once phase 1's MFMAs have been issued
           rdA(Aa, sl ^ 1, 0, 0);
@@ -462,33 +506,21 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         }
         __builtin_amdgcn_sched_barrier(0);
       } else {
-      if (t + 1 < nk) {
-        rdA(Aa, sl ^ 1, 0, 0);
-        rdB(Ba, sl ^ 1, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (SPREAD && !TAIL) {
-        if constexpr (VJ_GEMM_SPREAD == 2) {  // the A pieces after the first m-tile's MFMAs as well
-          mm_rows(Ab, 1, Bb, 0, 1);
-          __builtin_amdgcn_sched_barrier(0);
-          if (DMAW == 8 || wave < DMAW)
-            stage<AK, BM, false, DMAW, BK, WNX>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff, smem + sl * STAGE,
-                                                 wave, lane);
-          __builtin_amdgcn_sched_barrier(0);
-          mm_rows(Ab, 1, Bb, 1, 2);
-        } else {
-          mm_rows(Ab, 1, Bb, 0, SPLIT_AT);
+        if (t + 1 < nk) {
+          rdA(Aa, sl ^ 1, 0, 0);
+          rdB(Ba, sl ^ 1, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (b_iss)
-          stage<BKM, BN, DIRECT, DMAW, BK, WNX>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
-                                                 smem + sl * STAGE + A_BYTES, bwv, lane);
+        if constexpr (SPREAD && !TAIL) {
+          mm_rows(Ab, 1, Bb, 0, SPLIT);
+          __builtin_amdgcn_sched_barrier(0);
+          b_pieces();
+          __builtin_amdgcn_sched_barrier(0);
+          mm_rows(Ab, 1, Bb, SPLIT, MH);
+        } else {
+          mm(Ab, 1, Bb);
+        }
         __builtin_amdgcn_sched_barrier(0);
-        mm_rows(Ab, 1, Bb, VJ_GEMM_SPREAD == 2 ? 2 : SPLIT_AT, MH);
-      } else {
-        mm(Ab, 1, Bb);
-      }
-      __builtin_amdgcn_sched_barrier(0);
       }
     };
     int t = 0;
@@ -503,29 +535,16 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
 #endif
     int lane_e = lane;
     asm volatile("" : "+v"(lane_e));
-#if VJ_GEMM_NO_EPI  // measurement build: main loop only (the accumulators feed one never-taken store)
-    if (true) {
-      float sum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 2 * MH; ++i)
-#pragma unroll
-        for (int j = 0; j < NTN; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-      if (sum == 1.2345e-30f && g.C) ((float*)g.C)[lane_e] = sum;
-      if (has_next && !EARLY1) {
-        __syncthreads();
-        const Tile nxt = make_tile(wgn);
-        if (nxt.nk > 1) load_tile(nxt, 1, sle, lane_e);
-      }
-    } else
-#endif
     if constexpr (DIRECT) {
       const int lane = lane_e;
-      // ---- direct epilogue (K-major B staged with PERM): lane (c = lane&15, g = lane>>4) owns rows
-      // i*16 + 4g + r of m-tile i and the NTN consecutive columns nb .. nb+NTN-1, so every row goes
-      // out of registers as one 8/16-B store; no LDS round trip.
-      const int nb = cur.n0 + wc * WN + NTN * (lane & 15);
+      const int lrow = M32 ? 4 * (lane >> 5) : 4 * (lane >> 4);  // the lane's row offset in a virtual m-tile
+      // ---- direct epilogue (K-major B staged with PERM): lane (c = lane&15, g = lane>>4; 32x32x16:
+      // c = lane&31, g = lane>>5) owns rows rowoff(i) + 4g + r of virtual m-tile i and the NTN
+      // consecutive columns nb .. nb+NTN-1, so every row goes out of registers as one 8/16-B store;
+      // no LDS round trip.
+      const int nb = cur.n0 + wc * WN + NTN * (M32 ? (lane & 31) : (lane & 15));
       const bool nok = nb < g.N;
-      const int mb = cur.m0 + wr * WM + 4 * (lane >> 4);
+      const int mb = cur.m0 + wr * WM + lrow;
       float bias[NTN];
 #pragma unroll
       for (int j = 0; j < NTN; ++j) bias[j] = 0.f;
@@ -558,12 +577,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // AUX_PF m-tiles of rows in flight. Stamped (tools/gemm_stamps.py): the residual epilogue takes
       // ~36k cycles per tile vs ~10k without the reads, but deeper prefetch (3, 5, 7) measured no
       // faster: the 64 MB of residual every CU reads at once is the bound, not the latency chain
-      constexpr int AUX_PF = VJ_GEMM_AUX_PF;
       [[maybe_unused]] float aux[AUX_PF + 1][4][NTN];
       auto fetch = [&](int i, float (&dst)[4][NTN]) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = mb + i * 16 + r;
+          const int m = mb + rowoff(i) + r;
           const bool ok = m < g.M && nok;
           const long off = ok ? (long)m * g.ldaux + nb : 0;
           if constexpr (EPI == EPI_F32_RESID) {
@@ -602,13 +620,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int r = odd ? 2 + h : h;
-          const int m = mb + i * 16 + r;
+          const int m = mb + rowoff(i) + r;
           if (m < g.M && nok8) {
             const uint4 v = odd ? make_uint4(rcv[2 * h], rcv[2 * h + 1], pk[r][0], pk[r][1])
                                 : make_uint4(pk[r][0], pk[r][1], rcv[2 * h], rcv[2 * h + 1]);
-#if VJ_GEMM_NO_STORE
-            if (v.x == 0x12345u)
-#endif
             *(uint4*)(base + (long)m * ld + nb8) = v;
           }
         }
@@ -630,37 +645,38 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         }
         if constexpr (F32OUT && NTN == 4) {
           // f32 rows stored from the accumulators themselves: a 4x4 in-place transpose (tied swaps)
-          // turns acc[i][r] into row r's 4 columns, bias / residual are added in place (tied adds).
-          // Stores read their data registers after issue, so staging copies recycled from row to row
-          // cost one memory latency per 16-B store; the accumulators are not reused before the next tile.
+          // turns accv(i, r, 0..3) into row r's 4 columns, bias / residual are added in place (tied
+          // adds). Stores read their data registers after issue, so staging copies recycled from row
+          // to row cost one memory latency per 16-B store; the accumulators are not reused before the
+          // next tile. (32x32x16: row r's columns are then 4 consecutive registers of acc32[..][r].)
 #pragma unroll
           for (int a = 0; a < 4; ++a)
 #pragma unroll
             for (int b = a + 1; b < 4; ++b) {
-              float x = acc[i][a][b], y = acc[i][b][a];
+              float x = accv(i, a, b), y = accv(i, b, a);
               asm volatile("v_swap_b32 %0, %1" : "+v"(x), "+v"(y));
-              acc[i][a][b] = x;
-              acc[i][b][a] = y;
+              accs(i, a, b, x);
+              accs(i, b, a, y);
             }
 #pragma unroll
           for (int r = 0; r < 4; ++r)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float x = acc[i][r][e];
+              float x = accv(i, r, e);
               asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(bias[e]));
               if constexpr (EPI == EPI_F32_RESID) asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(aux[i % (AUX_PF + 1)][r][e]));
-              acc[i][r][e] = x;
+              accs(i, r, e, x);
             }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int m = mb + i * 16 + r;
+            const int m = mb + rowoff(i) + r;
             if (m < g.M && nok) {
               float* dst = EPI == EPI_PARTIAL ? g.ws + ((long)cur.z * g.M + m) * g.N + nb
                                               : (float*)g.C + (long)m * g.ldc + nb;
-#if VJ_GEMM_NO_STORE
-              if (acc[i][r][0] == 1.2345e-30f)
-#endif
-              *(f32x4*)dst = acc[i][r];
+              if constexpr (M32)
+                *(f32x4*)dst = f32x4{accv(i, r, 0), accv(i, r, 1), accv(i, r, 2), accv(i, r, 3)};
+              else
+                *(f32x4*)dst = acc[i][r];
             }
           }
           continue;
@@ -668,12 +684,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         [[maybe_unused]] uint32_t pk[4][2], ga[4][2];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = mb + i * 16 + r;
+          const int m = mb + rowoff(i) + r;
           float v[NTN];
 #pragma unroll
-          for (int j = 0; j < NTN; ++j) v[j] = acc[i][j][r] + bias[j];
+          for (int j = 0; j < NTN; ++j) v[j] = accv(i, j, r) + bias[j];
           if constexpr (EPI == EPI_ROPE) {
-            const int rp = rpos[wr * WM + i * 16 + 4 * (lane >> 4) + r];
+            const int rp = rpos[wr * WM + rowoff(i) + lrow + r];
 #pragma unroll
             for (int p = 0; p < NTN / 2; ++p) {
               if (!ract[p]) continue;
@@ -692,9 +708,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
             if (m < g.M && nok) {
               float* dst = EPI == EPI_PARTIAL ? g.ws + ((long)cur.z * g.M + m) * g.N + nb
                                               : (float*)g.C + (long)m * g.ldc + nb;
-#if VJ_GEMM_NO_STORE  // measurement build: the epilogue without its global stores
-              if (v[0] == 1.2345e-30f)
-#endif
               *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
             }
           } else {
@@ -869,22 +882,8 @@ int num_cus() {
 
 // Persistent grid: one block per CU (capped by the tile count), a multiple of 8 so every XCD gets
 // the same number of blocks. VJ_GEMM_PXCD caps the blocks per XCD (tests: many tiles per block).
-// Phase offset between the blocks of an XCD (experiment): odd blocks start later so that their
-// epilogues (HBM-bound) fall under the even blocks' main loops. VJ_GEMM_STAGGER = sleep units per
-// 1024 of K.
-int stagger_units(int K) {
-  const char* e = getenv("VJ_GEMM_STAGGER");
-  const int u = e ? atoi(e) : 0;
-  return u > 0 ? (int)((long)u * K / 1024) : 0;
-}
-
-// VJ_GEMM_BN256=1 (experiment): 256-wide tiles (direct-store epilogue) also when N % 256 != 0, the
-// last column tile partly empty, instead of 128-wide tiles with the LDS-staged epilogue
-int force_bn256() {
-  const char* e = getenv("VJ_GEMM_BN256");
-  return (e && e[0] == '1') ? 1 : 0;
-}
-
+// (A phase offset between the blocks of an XCD, so odd blocks' epilogues fall under the even
+// blocks' main loops, measured no gain in round 3 and was removed.)
 int grid256(long nb, int per_cu = 1) {
   int per_xcd = per_cu * num_cus() / 8;
   const char* e = getenv("VJ_GEMM_PXCD");
@@ -898,7 +897,7 @@ int grid256(long nb, int per_cu = 1) {
 // shares fewer A / B panels in its L2. Measured (tools/bench_kernels.py, MI355X): groups of 8 rows
 // pay on tall problems (target fc1 M = 49152: -7 %, predictor fc1 / fc2 / dgrad M = 71232: -3..-10 %)
 // and cost 2-5 % on the ~46-row-tile context problems, hence the tiles_m threshold.
-// VJ_GEMM_GROUP overrides (0 = row-major).
+// VJ_GEMM_GROUP overrides (0 = row-major; tests: grouped order at small sizes).
 int tile_group(int tiles_m, int tiles_n) {
   const char* e = getenv("VJ_GEMM_GROUP");
   if (e) return atoi(e) > 0 ? atoi(e) : 0;
@@ -909,7 +908,6 @@ int tile_group(int tiles_m, int tiles_n) {
 template <int BN>
 int launch256_f8(int epi, const G256& g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
-  const_cast<G256&>(g).stagger = stagger_units(2 * g.K);
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((k_gemm256<true, true, EPI_BF16, BN, true>), grid, dim3(512), 0, st, g); break;
     case EPI_F32: hipLaunchKernelGGL((k_gemm256<true, true, EPI_F32, BN, true>), grid, dim3(512), 0, st, g); break;
@@ -938,7 +936,6 @@ int use_2w(bool narrow) {
 
 int launch2w(int epi, G256 g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n, 2));
-  g.stagger = stagger_units(g.kslice);
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((k_gemm256<true, true, EPI_BF16, 128, false, 4>), grid, dim3(256), 0, st, g); break;
     case EPI_F32: hipLaunchKernelGGL((k_gemm256<true, true, EPI_F32, 128, false, 4>), grid, dim3(256), 0, st, g); break;
@@ -959,10 +956,9 @@ int launch2w(int epi, G256 g, hipStream_t st) {
   return VJ_OK;
 }
 
-// one-tile launch; 192-row tiles (BMT = 192) for the K-major 256-wide shapes vm192() picks
+// one-tile launch; 192-row tiles (BMT = 192) for the K-major 256-wide shapes use_bm192() picks
 int launch192(int epi, const G256& g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
-  const_cast<G256&>(g).stagger = stagger_units(g.kslice);
 #define L192(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 192>), grid, dim3(512), 0, st, g); break
   switch (epi) {
     case EPI_BF16: L192(EPI_BF16);
@@ -995,10 +991,38 @@ bool use_bm192(int M, int tn) {
   return r192 * 192 * 108 < r256 * 256 * 85;
 }
 
+// 32x32x16 form of the 256 x 256 tile (K-major A and B)
+int launch32(int epi, const G256& g, hipStream_t st) {
+  const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
+#define L32(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 256, true>), grid, dim3(512), 0, st, g); break
+  switch (epi) {
+    case EPI_BF16: L32(EPI_BF16);
+    case EPI_F32: L32(EPI_F32);
+    case EPI_F32_RESID: L32(EPI_F32_RESID);
+    case EPI_GELU: L32(EPI_GELU);
+    case EPI_GELU_BWD: L32(EPI_GELU_BWD);
+    case EPI_ROPE: L32(EPI_ROPE);
+    case EPI_BF16_RESID: L32(EPI_BF16_RESID);
+    default: vj_set_error("gemm256(32x32x16): bad epilogue %d", epi); return VJ_ERR_ARG;
+  }
+#undef L32
+  VJ_LAUNCH_CHECK("vj_gemm256(32x32x16)");
+  return VJ_OK;
+}
+
+// MFMA form of a K-major 256 x 256-tile GEMM. VJ_GEMM_MF: 16 = always 16x16x32, 32 = always 32x32x16
+// (where the shape takes 256-row tiles), unset = the measured default (GEMM).
+bool use_m32(int epi) {
+  const char* e = getenv("VJ_GEMM_MF");
+  if (e && e[0] == '3') return true;
+  if (e && e[0] == '1') return false;
+  (void)epi;
+  return false;
+}
+
 template <bool AK, bool BKM, int BN>
 int launch256(int epi, const G256& g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n * g.nsplit));
-  const_cast<G256&>(g).stagger = stagger_units(g.kslice);
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_BF16, BN>), grid, dim3(512), 0, st, g); break;
     case EPI_F32: hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_F32, BN>), grid, dim3(512), 0, st, g); break;
@@ -1028,11 +1052,6 @@ int launch256(int epi, const G256& g, hipStream_t st) {
 
 }  // namespace
 
-int vj_gemm_pp_mode(int epi);
-int vj_gemm_pp_dispatch(int M, int N, int K, const void* A, long lda, const void* B, long ldb, int epi,
-                        const float* bias, const void* aux, long ldaux, void* C, long ldc, void* C2, long ldc2,
-                        hipStream_t st, const void* rope, int group, int grid, int mode);
-
 // Called by vj_gemm_bf16_splitk (splitk == 1) when the problem suits a 256-row tile; arguments
 // already validated there. Returns VJ_ERR_UNSUPPORTED when it declines.
 int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
@@ -1042,17 +1061,9 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
     return VJ_ERR_UNSUPPORTED;
   if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
     return VJ_ERR_UNSUPPORTED;
-  // K-major A and B: the ping-pong kernel (vj_gemm_pp.hip) when it takes the shape
-  const int ppm = a_kmajor && b_kmajor ? vj_gemm_pp_mode(epi) : 0;
-  if (ppm) {
-    const int tm = vj_cdiv(M, 256), tn = vj_cdiv(N, 128);
-    const int rc = vj_gemm_pp_dispatch(M, N, K, A, lda, B, ldb, epi, bias, aux, ldaux, C, ldc, C2, ldc2, st, rope,
-                                       tile_group(tm, tn), grid256((long)tm * tn), ppm);
-    if (rc != VJ_ERR_UNSUPPORTED) return rc;
-  }
   // 256-wide tiles (direct-store epilogue) unless the last column tile would waste > 15 % of the work
   // (measured, tools/bench_kernels.py: predictor QKV N = 1152 -17 % with 256-wide tiles; N = 384 +14 %)
-  const bool wide = N % 256 == 0 || (N > 256 && (vj_cdiv(N, 256) * 256L * 100 <= 115L * N || force_bn256()));
+  const bool wide = N % 256 == 0 || (N > 256 && vj_cdiv(N, 256) * 256L * 100 <= 115L * N);
   const int bn = wide ? 256 : 128;
   const int tm = vj_cdiv(M, 256), tn = vj_cdiv(N, bn);
   G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, C, ldc, C2, ldc2, bias, aux, ldaux,
@@ -1073,6 +1084,7 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
       g.group = tile_group(g.tiles_m, tn);
       return launch192(epi, g, st);
     }
+    if (a_kmajor && b_kmajor && use_m32(epi)) return launch32(epi, g, st);
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
     if (a_kmajor && !b_kmajor) return launch256<true, false, 256>(epi, g, st);
     if (!a_kmajor && b_kmajor) return launch256<false, true, 256>(epi, g, st);

@@ -1,5 +1,4 @@
-// Shared device helpers of the 256-row bf16 / fp8 GEMM kernels (vj_gemm256.hip: one tile per
-// workgroup; vj_gemm_pp.hip: two wave groups in ping-pong): the kernel argument block, LDS-DMA
+// Device helpers of the 256-row bf16 / fp8 GEMM kernel (vj_gemm256.hip): the kernel argument block, LDS-DMA
 // staging of K-major / MN-major operand tiles with the XOR swizzles, MFMA fragment reads and the
 // GELU epilogue pair. Everything sits in an anonymous namespace: each translation unit compiles
 // its own copy (no cross-TU codegen coupling of the kernels).
@@ -7,18 +6,6 @@
 #include "vj_common.h"
 
 namespace {
-
-// m-tiles of residual / saved-derivative rows the direct epilogue keeps in flight
-#ifndef VJ_GEMM_AUX_PF
-#define VJ_GEMM_AUX_PF 1
-#endif
-// Waves that issue the LDS-DMA of a K stage: 8 (all) or 4 (waves 0-3, so their SIMD partners 4-7
-// keep the matrix pipe busy while the DMA issues; k_gemm256 applies it to its 256-wide bf16 tiles
-// without a VALU-heavy epilogue). Measured (profiles/r03_gemm_dmaw4_kernels.txt): those shapes
-// -1.5..-7 %, step +0.1..0.3 % (three same-call A/Bs).
-#ifndef VJ_GEMM_DMA_WAVES
-#define VJ_GEMM_DMA_WAVES 4
-#endif
 
 // epilogue numbering: vj_common.h (EPI_BF16_RESID: the no-grad target encoder's residual stream in the
 // reference's own autocast precision, x = x + proj(...) in bf16, half the epilogue bytes of F32_RESID)
@@ -48,7 +35,6 @@ struct G256 {
   // scales: A(m, k) = a8 * 2^ea[m], B(n, k) = b8 * 2^eb[n] (E8M0 scale operands of the MFMA)
   const int* ea = nullptr;
   const int* eb = nullptr;
-  int stagger = 0;  // s_sleep(32) units odd blocks of an XCD wait before their first tile
 };
 
 constexpr int BK = 64;
@@ -66,11 +52,12 @@ __device__ __forceinline__ int mn_swz(int k) { return 2 * (k & 3) + 8 * ((k >> 3
 
 // K-major image: [ROWS][64] bf16, 128-B rows, chunk ^= (row>>1)&7.
 // MN-major image: [64][ROWS] bf16, ROWS*2-B rows, chunk ^= mn_swz(k).
-// PERM (K-major B only): LDS row r of each WN-row group holds global row NTN*(r%16) + r/16 of the
-// group, so n-tile j of the MFMA accumulators covers the group's columns {NTN*c + j}: each lane
-// then owns NTN CONSECUTIVE output columns and the epilogue stores straight from registers.
+// PERM (K-major B only): LDS row r of each WN-row group holds global row NTN*(r%PB) + r/PB of the
+// group (PB = the MFMA output block width, 16 or 32; NTN = WN / PB), so n block j of the MFMA
+// accumulators covers the group's columns {NTN*c + j}: each lane then owns NTN CONSECUTIVE output
+// columns and the epilogue stores straight from registers.
 // NW waves issue the tile's 1-KB pieces (waves 0 .. NW-1).
-template <bool KMAJ, int ROWS, bool PERM = false, int NW = 8, int BKT = 64, int WNX = 4>
+template <bool KMAJ, int ROWS, bool PERM = false, int NW = 8, int BKT = 64, int WNX = 4, int PB = 16>
 __device__ __forceinline__ void stage(__amdgpu_buffer_rsrc_t rs, long ld, int rows_left, int k0, int K,
                                       LDS_AS char* lds, int wave, int lane) {
   constexpr int PIECES = ROWS * BKT * 2 / 1024;  // 1-KB DMA pieces per operand tile
@@ -88,9 +75,9 @@ __device__ __forceinline__ void stage(__amdgpu_buffer_rsrc_t rs, long ld, int ro
       const int kk = k0 + c * 8;
       int gr = r;
       if constexpr (PERM) {
-        constexpr int WN = ROWS / WNX, NTN = WN / 16;
+        constexpr int WN = ROWS / WNX, NTN = WN / PB;
         const int rl = r % WN;
-        gr = (r - rl) + NTN * (rl & 15) + (rl >> 4);
+        gr = (r - rl) + NTN * (rl % PB) + (rl / PB);
       }
       voff = (gr < rows_left && kk < K) ? (uint32_t)(((long)gr * ld + kk) * 2) : VJ_OOB;
     } else {

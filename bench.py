@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--kernel-events", type=int, default=1)
     ap.add_argument("--fp8-target", type=int, default=0, help="target encoder QKV / fc1 GEMMs on the fp8 MFMA")
+    ap.add_argument("--synced-steps", type=int, default=5,
+                    help="untimed comparison steps with a float(loss) host sync per step (0: skip)")
     args = ap.parse_args()
     if args.gpus > 1 and "RANK" not in os.environ:
         # no launcher: start one rank process per GPU from this GPU-free parent
@@ -93,6 +95,9 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} rank(s)")
     dev = torch.device("cuda", local_rank)
+    # every rank states its process group (RCCL carried the buckets iff backend == "nccl")
+    print(f"[bench rank {rank}/{world}] backend={dist.get_backend() if world > 1 else None} device={dev}",
+          file=sys.stderr, flush=True)
     B, T, S = args.batch, args.frames, args.crop
     N = (T // 2) * (S // 16) ** 2
 
@@ -153,6 +158,8 @@ def main():
     # step-boundary events on the compute stream (no host sync between steps): per-step times for
     # the median; the contract's ms_per_step stays wall-clock over the K steps
     marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    trainer.time_allreduce = True  # two events per step on the compute stream (no host sync)
+    trainer.ar_events.clear()
     t0 = time.perf_counter()
     marks[0].record()
     for i in range(args.warmup, nsteps):
@@ -162,6 +169,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    trainer.time_allreduce = False
     if prof:
         prof.stop()
     if world > 1:
@@ -176,6 +184,14 @@ def main():
         t = torch.tensor([ms_median], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms_median = t.item()
+    # exposed all-reduce: backward end -> GradReducer.finish() end, median over the timed steps, max
+    # over ranks (0 at world 1: there is no reducer)
+    ar = sorted(a.elapsed_time(b) for a, b in trainer.ar_events)
+    ar_ms = (ar[len(ar) // 2] if len(ar) % 2 else 0.5 * (ar[len(ar) // 2 - 1] + ar[len(ar) // 2])) if ar else 0.0
+    if world > 1:
+        t = torch.tensor([ar_ms], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ar_ms = t.item()
     total_clips = B * world * args.steps
     value = total_clips / elapsed
     flops = sum(step_flops(args.model, B, N, d[1], d[2]) for d in data[args.warmup:]) / args.steps
@@ -216,6 +232,27 @@ def main():
                             "avg_launch_us": round(st1["total_ms"] * 1e3 / st1["count"], 2),
                             "measured": "one extra untimed step, target encoder on the main stream"}
 
+    # Untimed comparison (not the headline): the same steps with the reference loop's per-step host
+    # sync (float(loss) every iteration, app/vjepa/train.py:468), to state what the free-running
+    # timed loop above leaves out.
+    synced = None
+    if args.synced_steps > 0:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for i in range(args.synced_steps):
+            float(run(args.warmup + i % args.steps))
+        torch.cuda.synchronize()
+        te = time.perf_counter() - ts
+        if world > 1:
+            t = torch.tensor([te], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            te = t.item()
+        synced = {"ms_per_step": round(te * 1e3 / args.synced_steps, 2), "steps": args.synced_steps,
+                  "sync": "float(loss) after every step (app/vjepa/train.py:468); untimed for value",
+                  "vs_free_running": round(te * 1e3 / args.synced_steps / ms, 4)}
+
     cpu = None
     if rank == 0 and args.cpu_baseline:
         cpu = cpu_baseline(args, data[0])
@@ -235,7 +272,8 @@ def main():
                "dist_backend": dist.get_backend() if world > 1 else None, "step_tflop": round(flops / 1e12, 2),
                "step_tflops_per_gpu": round(flops / (ms * 1e-3) / 1e12, 1),
                "mfu_bf16": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-               "loss_last": round(float(loss.item()), 5), "roofline": roof, "cpu_baseline": cpu}
+               "loss_last": round(float(loss.item()), 5), "allreduce_exposed_ms": round(ar_ms, 3),
+               "synced_comparison": synced, "roofline": roof, "cpu_baseline": cpu}
         if kstats:  # one untimed warmup step, every launch timed
             out["kernels"] = {k: {"ms_per_step": round(v["total_ms"], 3), "count_per_step": v["count"],
                                   "tflops": round(v["flops"] / (v["total_ms"] * 1e-3) / 1e12, 1) if v["flops"] else None}

@@ -94,4 +94,10 @@ def test_bench_gpus2_spawns_two_ranks():
     assert out["dist_backend"] == "gloo"
     assert abs(out["clips_per_s_per_gpu"] * 2 - out["value"]) < 1e-2 * out["value"]
     assert out["ms_per_step_median"] > 0
+    # the exposed all-reduce time (backward end -> GradReducer.finish() end, median, max over ranks)
+    # and every rank's process-group report
+    assert out["allreduce_exposed_ms"] >= 0
+    assert out["synced_comparison"]["ms_per_step"] > 0
+    for rk in (0, 1):
+        assert f"[bench rank {rk}/2] backend=gloo" in r.stderr, r.stderr[-2000:]
     print(lines[0][:400])

@@ -139,6 +139,11 @@ class JEPATrainer:
         self.enc_arenas = [enc_w, enc_n]
         self.mask_tokens = list(self.pred.mask_tokens) if self.pred.mask_tokens is not None else []
         self.reducer = None
+        # time_allreduce: per step, a HIP event pair on the compute stream from the end of the backward
+        # (last gradient written) to the end of GradReducer.finish() (the stream waits for every
+        # bucket): the all-reduce time NOT hidden under the backward. Appended to ar_events.
+        self.time_allreduce = False
+        self.ar_events = []
         if world_size > 1:
             seg = lambda a: (a.grad, [(p, o, p.numel()) for p, o in zip(a.params, a.offsets)])  # noqa: E731
             self.reducer = GradReducer([seg(pred_w), seg(enc_w)], tail_segments=[seg(pred_n), seg(enc_n)],
@@ -219,8 +224,15 @@ class JEPATrainer:
         self._groups = G
         for a in self.opt.arenas:  # lazily zeroed gradients nothing wrote (before the tail buckets)
             a.finalize_grads()
+        ev = None
+        if self.time_allreduce:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         if self.reducer is not None:
             self.reducer.finish()
+        if ev is not None:
+            ev[1].record()
+            self.ar_events.append(ev)
         return total
 
     def apply_update(self, momentum):

@@ -317,9 +317,15 @@ def test_attention_rescale_spikes(hd):
 
 
 # ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("fwd", ["default", "1"])
 @pytest.mark.parametrize("D", [64, 384, 1024, 1408])
-def test_layernorm(D):
+def test_layernorm(D, fwd, monkeypatch):
+    """LayerNorm forward (k_ln_fwd3: all rows of a wave in flight; VJ_LN_FWD=1 and f32 rows wider
+    than 1024: k_ln_fwd) and backward vs torch, f32 / bf16 inputs and outputs."""
     from vjepa2_amd import ops
+
+    if fwd != "default":
+        monkeypatch.setenv("VJ_LN_FWD", fwd)
 
     g = torch.Generator(device="cpu").manual_seed(D)
     M = 301

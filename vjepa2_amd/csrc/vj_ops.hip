@@ -135,53 +135,51 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int M, int D, const void* __rest
   }
 }
 
-// LayerNorm forward, persistent: each wave walks rows w, w + W, ... (W = waves in the grid) with the
-// next row's loads issued before the current row's reductions; every lane moves 16 B per access
-// (E = 8 bf16 or 4 f32 elements of x; the bf16 output row goes out as 16-B / 8-B stores), and the
-// affine parameters are loaded once per wave. Element map: vector i of lane l holds the E elements
-// (64 i + l) E ... Replaces k_ln_fwd for the bf16 / f32 outputs (the fp8 output keeps k_ln_fwd).
-template <bool XBF, bool YF32, int NV>
-__global__ __launch_bounds__(256) void k_ln_fwd2(int M, int D, const void* __restrict__ x, long ldx,
+// LayerNorm forward with every row of a wave in flight at once: a wave owns R consecutive rows and
+// issues all their 16-B loads (E = 8 bf16 or 4 f32 elements per lane-vector, kept packed as loaded)
+// before the first reduction, so a CU holds R x the bytes in flight of a one-row-lookahead loop at
+// a lower register cost (bf16 rows stay packed: 8 VGPRs per 1024-wide row). Element map: vector i of
+// lane l holds elements (64 i + l) E ... + E - 1. Outputs: bf16 rows as 16-B (E = 8) / 8-B stores,
+// f32 rows as 16-B stores; gamma / beta re-read per row (L1 hits) instead of held in registers.
+template <bool XBF, bool YF32, int NV, int R>
+__global__ __launch_bounds__(256) void k_ln_fwd3(int M, int D, const void* __restrict__ x, long ldx,
                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
                                                  float eps, void* __restrict__ y, long ldy, float* __restrict__ mean,
                                                  float* __restrict__ rstd) {
   constexpr int E = XBF ? 8 : 4;
   const int lane = threadIdx.x & 63;
-  const long W = (long)gridDim.x * 4;
-  long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  float g[NV][E], bb[NV][E], v[NV][E], vn[NV][E];
+  const long row0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= M) return;
   auto ok = [&](int i) { return (i * 64 + lane) * E < D; };
-  auto load = [&](long r, float (&dst)[NV][E]) {
+  uint4 raw[R][NV];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      if (!ok(i)) continue;
-      const long off = r * ldx + (i * 64 + lane) * E;
-      if constexpr (XBF) {
-        const uint4 u = *(const uint4*)((const bf16_t*)x + off);
-        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          dst[i][2 * k] = __builtin_bit_cast(float, w[k] << 16);
-          dst[i][2 * k + 1] = __builtin_bit_cast(float, w[k] & 0xffff0000u);
-        }
-      } else {
-        const float4 f = *(const float4*)((const float*)x + off);
-        dst[i][0] = f.x; dst[i][1] = f.y; dst[i][2] = f.z; dst[i][3] = f.w;
+      raw[r][i] = make_uint4(0u, 0u, 0u, 0u);
+      if (ok(i) && row0 + r < M) {
+        const long off = (row0 + r) * ldx + (i * 64 + lane) * E;
+        raw[r][i] = XBF ? *(const uint4*)((const bf16_t*)x + off) : *(const uint4*)((const float*)x + off);
       }
     }
-  };
 #pragma unroll
-  for (int i = 0; i < NV; ++i)
+  for (int r = 0; r < R; ++r) {
+    const long row = row0 + r;
+    if (row >= M) break;
+    float v[NV][E];
 #pragma unroll
-    for (int k = 0; k < E; ++k) {
-      const int c = (i * 64 + lane) * E + k;
-      g[i][k] = gamma && ok(i) ? gamma[c] : 1.f;
-      bb[i][k] = gamma && ok(i) ? beta[c] : 0.f;
+    for (int i = 0; i < NV; ++i) {
+      const uint32_t w[4] = {raw[r][i].x, raw[r][i].y, raw[r][i].z, raw[r][i].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if constexpr (XBF) {
+          v[i][2 * k] = __builtin_bit_cast(float, w[k] << 16);
+          v[i][2 * k + 1] = __builtin_bit_cast(float, w[k] & 0xffff0000u);
+        } else {
+          v[i][k] = __builtin_bit_cast(float, w[k]);
+        }
+      }
     }
-  load(row, v);
-  for (; row < M; row += W) {
-    if (row + W < M) load(row + W, vn);
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < NV; ++i)
@@ -202,10 +200,19 @@ __global__ __launch_bounds__(256) void k_ln_fwd2(int M, int D, const void* __res
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       if (!ok(i)) continue;
+      const int c = (i * 64 + lane) * E;
       float o[E];
 #pragma unroll
-      for (int k = 0; k < E; ++k) o[k] = (v[i][k] - mu) * rs * g[i][k] + bb[i][k];
-      const long off = row * ldy + (i * 64 + lane) * E;
+      for (int k = 0; k < E; ++k) o[k] = (v[i][k] - mu) * rs;
+      if (gamma) {
+#pragma unroll
+        for (int k = 0; k < E; k += 4) {
+          const float4 gg = *(const float4*)(gamma + c + k), bb = *(const float4*)(beta + c + k);
+          o[k] = o[k] * gg.x + bb.x; o[k + 1] = o[k + 1] * gg.y + bb.y;
+          o[k + 2] = o[k + 2] * gg.z + bb.z; o[k + 3] = o[k + 3] * gg.w + bb.w;
+        }
+      }
+      const long off = row * ldy + c;
       if constexpr (YF32) {
 #pragma unroll
         for (int k = 0; k < E; k += 4) *(float4*)((float*)y + off + k) = make_float4(o[k], o[k + 1], o[k + 2], o[k + 3]);
@@ -220,10 +227,6 @@ __global__ __launch_bounds__(256) void k_ln_fwd2(int M, int D, const void* __res
       if (mean) mean[row] = mu;
       if (rstd) rstd[row] = rs;
     }
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-#pragma unroll
-      for (int k = 0; k < E; ++k) v[i][k] = vn[i][k];
   }
 }
 
@@ -1064,15 +1067,19 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
   VJ_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "vj_layernorm_fwd: gamma/beta both or neither");
   VJ_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "vj_layernorm_fwd: strides must be %%4");
   hipStream_t st = (hipStream_t)stream;
-  // the per-16-row-block kernel: measured faster than the persistent 16-B-access k_ln_fwd2 on every
-  // train-step shape (tools/bench_kernels.py: 43 vs 47 us target, 19 vs 23 us context, 30 vs 36 us
-  // predictor); VJ_LN_FWD2=1 selects k_ln_fwd2
-  const char* e = getenv("VJ_LN_FWD2");
-  if (!(e && e[0] == '1')) {
-    dim3 grid((M + 4 * LN_RPW - 1) / (4 * LN_RPW));
-    const int nv = ln_nv(D);
-#define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, YF, NVV>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
-#define LNF_NV(XB, YF) switch (nv) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 4: LNF(XB, YF, 4); break; case 6: LNF(XB, YF, 6); break; default: LNF(XB, YF, 8); }
+  // k_ln_fwd3 (all rows of a wave in flight, 16-B accesses) where the row fits its register budget and
+  // the strides allow 16-B vectors; else the one-row-lookahead k_ln_fwd. VJ_LN_FWD=1 forces k_ln_fwd
+  // (A/B). (Round 3's persistent 16-B variant k_ln_fwd2 measured slower than k_ln_fwd and was removed.)
+  const int E = x_bf16 ? 8 : 4;
+  const int nv3 = (D + 64 * E - 1) / (64 * E);
+  const char* e = getenv("VJ_LN_FWD");
+  const bool v3 = !(e && e[0] == '1') && D % E == 0 && ldx % E == 0 && ldy % (y_f32 ? 4 : E) == 0 && nv3 <= 4 &&
+                  !((uintptr_t)x & 15) && !((uintptr_t)y & 15) && !((uintptr_t)gamma & 15) && !((uintptr_t)beta & 15);
+  if (v3) {
+    constexpr int R = 4;
+    dim3 grid((M + 4 * R - 1) / (4 * R));
+#define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd3<XB, YF, NVV, R>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
+#define LNF_NV(XB, YF) switch (nv3) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 3: LNF(XB, YF, 3); break; default: LNF(XB, YF, 4); }
     if (x_bf16 && y_f32) { LNF_NV(true, true) }
     else if (x_bf16) { LNF_NV(true, false) }
     else if (y_f32) { LNF_NV(false, true) }
@@ -1082,15 +1089,10 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
     VJ_LAUNCH_CHECK("vj_layernorm_fwd");
     return VJ_OK;
   }
-  // persistent: 4 blocks of 4 waves per CU (all resident at <= 128 VGPRs), fewer when M is small
-  const long want = ((long)M + 3) / 4;
-  const int grid = (int)(want < 256L * 4 ? want : 256L * 4);
-  const int E = x_bf16 ? 8 : 4;
-  const int nv = (D + 64 * E - 1) / (64 * E);  // 16-B vectors per lane
-  VJ_CHECK_ARG(D % E == 0 && ldx % E == 0 && nv <= 8, "vj_layernorm_fwd: D=%d, ldx must be %% %d", D, E);
-  VJ_CHECK_ARG(ldy % (y_f32 ? 4 : E) == 0, "vj_layernorm_fwd: ldy must be %% %d", y_f32 ? 4 : E);
-#define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd2<XB, YF, NVV>), dim3(grid), dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
-#define LNF_NV(XB, YF) switch (nv) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 3: LNF(XB, YF, 3); break; case 4: LNF(XB, YF, 4); break; case 6: LNF(XB, YF, 6); break; default: LNF(XB, YF, 8); }
+  dim3 grid((M + 4 * LN_RPW - 1) / (4 * LN_RPW));
+  const int nv = ln_nv(D);
+#define LNF(XB, YF, NVV) hipLaunchKernelGGL((k_ln_fwd<XB, YF, NVV>), grid, dim3(256), 0, st, M, D, x, ldx, gamma, beta, eps, y, ldy, mean, rstd)
+#define LNF_NV(XB, YF) switch (nv) { case 1: LNF(XB, YF, 1); break; case 2: LNF(XB, YF, 2); break; case 4: LNF(XB, YF, 4); break; case 6: LNF(XB, YF, 6); break; default: LNF(XB, YF, 8); }
   if (x_bf16 && y_f32) { LNF_NV(true, true) }
   else if (x_bf16) { LNF_NV(true, false) }
   else if (y_f32) { LNF_NV(false, true) }

@@ -221,6 +221,24 @@ def ln_fwd_case(lib, M, D, xbf, dev, stream):
     return run, M * D * ((2 if xbf else 4) + 2) * 1e3
 
 
+# (name, M, N): bias-gradient column sums of a bf16 [M, N] gradient (qkv / fc1 of the context and
+# predictor blocks); TB/s of the bytes read
+CSUM = [("colsum ctx fc1", 11712, 4096), ("colsum ctx qkv", 11712, 3072), ("colsum pred fc1", 71232, 1536)]
+
+
+def colsum_case(lib, M, N, dev, stream):
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(M, N, generator=g).to(dev).bfloat16()
+    out = torch.zeros(N, device=dev)
+    ws = torch.empty(256 * N, device=dev)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def run():
+        rc = lib.vj_colsum_f32(M, N, p(x), 1, N, p(out), 0, p(ws), ws.numel(), stream)
+        assert rc == 0, rc
+    return run, M * N * 2 * 1e3
+
+
 def time_fn(fn, iters=10):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
@@ -279,6 +297,10 @@ def main():
         if (only and only not in name) or kind not in ("", "ln"):
             continue
         cases.append((name, [ln_fwd_case(lib, M, D, xbf, dev, stream) for lib in libs]))
+    for name, M, N in CSUM:
+        if (only and only not in name) or kind not in ("", "ln", "mem"):
+            continue
+        cases.append((name, [colsum_case(lib, M, N, dev, stream) for lib in libs]))
     for name, M, D, acc in LNB:
         if (only and only not in name) or kind not in ("", "ln"):
             continue

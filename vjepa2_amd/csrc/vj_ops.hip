@@ -465,22 +465,45 @@ __global__ __launch_bounds__(256) void k_colsum1(int M, int N, const void* __res
   const long r0 = (long)blockIdx.y * rows_per_slice;
   const long r1 = min((long)M, r0 + rows_per_slice);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (c0 < N) {
-    for (long r = r0 + rg; r < r1; r += 4) {
-      if constexpr (BF) {
-        const uint4 u = *(const uint4*)((const bf16_t*)x + r * ld + c0);
-        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  auto add = [&](const uint4 (&u)[BF ? 1 : 2]) {
+    if constexpr (BF) {
+      const uint32_t w[4] = {u[0].x, u[0].y, u[0].z, u[0].w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[2 * j] += bf2f(w[j] & 0xffff);
-          acc[2 * j + 1] += bf2f(w[j] >> 16);
-        }
-      } else {
-        const float4 a = *(const float4*)((const float*)x + r * ld + c0);
-        const float4 b = *(const float4*)((const float*)x + r * ld + c0 + 4);
-        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += bf2f(w[j] & 0xffff);
+        acc[2 * j + 1] += bf2f(w[j] >> 16);
       }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        acc[4 * h] += __uint_as_float(u[h].x); acc[4 * h + 1] += __uint_as_float(u[h].y);
+        acc[4 * h + 2] += __uint_as_float(u[h].z); acc[4 * h + 3] += __uint_as_float(u[h].w);
+      }
+    }
+  };
+  auto load = [&](long r, uint4 (&u)[BF ? 1 : 2]) {
+    if constexpr (BF) {
+      u[0] = *(const uint4*)((const bf16_t*)x + r * ld + c0);
+    } else {
+      u[0] = *(const uint4*)((const float*)x + r * ld + c0);
+      u[1] = *(const uint4*)((const float*)x + r * ld + c0 + 4);
+    }
+  };
+  if (c0 < N) {
+    // 4 rows per step with every load issued before the adds (4 x 16-32 B in flight per thread);
+    // the per-column add order stays the row order of this thread's rows
+    long r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      uint4 u[4][BF ? 1 : 2];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) load(r + 4 * k, u[k]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) add(u[k]);
+    }
+    for (; r < r1; r += 4) {
+      uint4 u[BF ? 1 : 2];
+      load(r, u);
+      add(u);
     }
   }
 #pragma unroll

@@ -74,18 +74,6 @@ int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k
                 long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
                 const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
                 const float* cos_t, const float* sin_t, void* stream);
-/* Backward with a workspace (bytes from vj_attn_bwd_ws_bytes): with VJ_ATTN_FUSED=1 in the
- * environment (opt-in: measured slower than the two sweeps), head dims 32 and 64 without a
- * frame-causal mask run the fused backward: the dK/dV sweep also multiplies each query tile's dS by
- * the block's K rows (dQ partial per 128-/256-key block, f32 in the workspace) and a reduce pass sums
- * the blocks in a fixed order, so S, P and dP are evaluated once per score instead of twice. Same
- * outputs as vj_attn_bwd_fc up to the dQ sum order; still deterministic. fblk > 0, head dims 80 / 88
- * and a NULL or short workspace take the two sweeps. */
-int vj_attn_bwd_ws_bytes(int H, int hd, int ngroups, const int* nseq, const int* len, long* bytes);
-int vj_attn_bwd_ws(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, const void* o,
-                   long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
-                   const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
-                   const float* cos_t, const float* sin_t, int fblk, void* ws, long ws_bytes, void* stream);
 /* Frame-causal (block-causal) variants for the action-conditioned predictor: with fblk > 0, token i
  * of a sequence attends to key j iff j / fblk <= i / fblk, i.e. F.scaled_dot_product_attention with the
  * attn_mask of build_action_block_causal_attention_mask (src/models/utils/modules.py:12-23; fblk = action

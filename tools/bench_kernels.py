@@ -154,17 +154,9 @@ def attn_case(lib, hd, H, groups, dev, stream, bwd):
         assert lib.vj_attn_fwd(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(stats), sc, len(groups), ns, ln, stream) == 0
     fwd()
 
-    nbytes = sum(n * H * l * ((l + 7) // 8 * 8) * 2 for n, l in groups)
-    ws = torch.empty(max(8, nbytes // 2), dtype=torch.bfloat16, device=dev)  # dS^T (used only with VJ_ATTN_DS=1)
-
     def bwdf():
-        fn = getattr(lib, "vj_attn_bwd_ws", None)
-        if fn is None:  # an older build
-            assert lib.vj_attn_bwd(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(do), D, P(stats), P(dqkv), 3 * D,
-                                   sc, len(groups), ns, ln, None, 0, 0, 0, None, None, stream) == 0
-            return
-        assert fn(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(do), D, P(stats), P(dqkv), 3 * D, sc, len(groups),
-                  ns, ln, None, 0, 0, 0, None, None, 0, P(ws), ws.numel() * 2, stream) == 0
+        assert lib.vj_attn_bwd(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(do), D, P(stats), P(dqkv), 3 * D,
+                               sc, len(groups), ns, ln, None, 0, 0, 0, None, None, stream) == 0
     fl = sum(4.0 * n * l * l * D for n, l in groups)
     return (bwdf, 2.5 * fl) if bwd else (fwd, fl)  # backward: FA2 convention, 5 matmuls
 

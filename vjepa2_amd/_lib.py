@@ -31,9 +31,6 @@ SIGNATURES = {
     "vj_attn_fwd_fc": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _F, _I, _P, _P, _I, _P],
     "vj_attn_bwd_fc": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _F, _I, _P, _P, _P, _I, _I, _I, _P,
                        _P, _I, _P],
-    "vj_attn_bwd_ws": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _F, _I, _P, _P, _P, _I, _I, _I, _P,
-                       _P, _I, _P, _L, _P],
-    "vj_attn_bwd_ws_bytes": [_I, _I, _I, _P, _P, _P],
     "vj_qkv_rope_gemm": [_I, _I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _I, _I, _I, _P, _P, _I, _P],
     "vj_layernorm_fwd": [_I, _I, _P, _I, _L, _P, _P, _F, _P, _I, _L, _P, _P, _P],
     "vj_gemm_fp8": [_I, _I, _I, _P, _L, _P, _P, _L, _P, _I, _P, _P, _L, _P, _L, _P, _L, _P],

@@ -25,46 +25,16 @@
 
 #include "vj_common.h"
 
-// 32-row key (dK/dV sweep) and query (dQ sweep) tiles per wave, per head dim
-#ifndef VJ_ATTN_KW32
-#define VJ_ATTN_KW32 2
-#endif
-#ifndef VJ_ATTN_QW32
-#define VJ_ATTN_QW32 2
-#endif
-#ifndef VJ_ATTN_KW64
-#define VJ_ATTN_KW64 1
-#endif
-#ifndef VJ_ATTN_QW64
-#define VJ_ATTN_QW64 1
-#endif
-
-// forward workgroups per CU the register budget is sized for (head dims <= 64)
-// forward, head dim 64: K / V^T fragments in rings (fewer live registers) at 4 workgroups per CU
-#ifndef VJ_ATTN_PRIO  // forward: s_setprio 1 around the S and PV MFMA clusters
-#define VJ_ATTN_PRIO 3
-#endif
-#ifndef VJ_ATTN_BPRIO  // backward sweeps: s_setprio 1 around the S / dP (bit 0) and dV / dK or dQ (bit 1) MFMAs
-#define VJ_ATTN_BPRIO 0
-#endif
-#ifndef VJ_ATTN_FWD_RING
-#define VJ_ATTN_FWD_RING 0
-#endif
-#ifndef VJ_ATTN_FWD_SPREAD
-#define VJ_ATTN_FWD_SPREAD 0
-#endif
-#ifndef VJ_ATTN_FWD_RING_V  // PV k-step after whose MFMAs the last two k-steps' V^T are read
-#define VJ_ATTN_FWD_RING_V 1
-#endif
-#ifndef VJ_ATTN_FWD_RING_OCC
-#define VJ_ATTN_FWD_RING_OCC 4
-#endif
-#ifndef VJ_ATTN_FWD32_OCC  // head dim 32 (predictor): 102 VGPRs hold 4 workgroups per CU
-#define VJ_ATTN_FWD32_OCC 3
-#endif
-#ifndef VJ_ATTN_FWD_OCC
-#define VJ_ATTN_FWD_OCC 3
-#endif
+// Launch shapes fixed by the round-2/3 measurements (attention; the variants were removed
+// from the source): 32-row key (dK/dV sweep) and query (dQ sweep) tiles per wave: 2 at head dim 32,
+// 1 otherwise; forward at 3 workgroups per CU (head dims <= 64) with s_setprio 1 around the head-dim-64
+// S and PV MFMA clusters; dQ sweep at 3 workgroups per CU for head dim 64. Measured slower and
+// removed: a K / V^T fragment ring at 4 forward workgroups per CU (spills), the V-tile DMA under the
+// softmax, priority around the backward MFMAs, the fused backward (dQ partials from the dK/dV sweep
+// plus a reduce pass; 192.7 vs 196.9 clips/s) and a separate delta kernel.
+constexpr int KW32 = 2, QW32 = 2, KW64 = 1, QW64 = 1;
+constexpr int FWD_OCC = 3;    // forward workgroups per CU the register budget is sized for (hd <= 64)
+constexpr int DQ64_OCC = 3;   // dQ sweep, head dim 64: 168 VGPRs (one dword reloaded per key tile)
 
 namespace {
 
@@ -75,7 +45,6 @@ struct SeqGroups {
   int len[MAXG];
   int tok0[MAXG];
   int tiles_prefix[MAXG + 1];  // cumulative tile counts (tile size set by the kernel)
-  long part_off[MAXG];         // fused backward: float offset of group g's dQ partials [seq][head][kblock]
 };
 
 struct AttnArgs {
@@ -101,12 +70,6 @@ struct AttnArgs {
   // (build_action_block_causal_attention_mask, modules.py:12-23, with fblk = cond tokens + H*W);
   // 0 = non-causal (every key of the sequence)
   int fblk;
-  // fused backward (k_attn_bwd_dkdv<HD, KW, true>): per key block, dQ partial = dS K over the block's
-  // keys, f32 [query][hd] per (sequence, head, key block) at part_off; k_attn_dq_reduce sums them
-  float* dqp;
-  // dQ sweep: computes delta = rowsum(dO * O) itself (from its dO fragments and O) and writes -delta to
-  // stats for the dK/dV sweep that runs after it (no separate k_attn_delta launch)
-  int dq_delta;
 };
 
 // key limit of query qloc (keys [0, klim) are visible) and its block-uniform bounds
@@ -304,52 +267,6 @@ __device__ __forceinline__ bf16x8 tr_frag_at(uint32_t lo, uint32_t hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// ---- 16x16x32 operand images of the fused dQ product (k_attn_bwd_dkdv<HD, KW, true>): key-major
-// rows of RB bytes (64: 32 bf16, 128: 64 bf16), 32-B column pairs XOR-swizzled by row so that a
-// transposed fragment read (per half-wave: 8 rows x 32 B at one column pair) hits every bank once.
-template <int RB>
-__device__ __forceinline__ int pair_swz(int r) {
-  return RB == 64 ? ((r >> 3) & 1) : (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
-}
-template <int RB>
-__device__ __forceinline__ int img_off(int r, int col) {  // byte offset of bf16 element col of row r
-  return r * RB + (((col >> 4) ^ pair_swz<RB>(r)) << 5) + ((col & 15) << 1);
-}
-// 16x16x32 MFMA operand from a key-major image X[k][m]: lane l holds X[kb + 8(l>>4) + j][mb + (l&15)],
-// j = 0..7 — the same key order for the A (K^T) and B (dS^T) operands, so the product sums the same
-// keys. The swizzle depends only on row bits 1 and 3, so for kb a multiple of 32 the address is the
-// lane part img_lane(mb) (computed once per use site) plus kb * RB. Asm reads: lds_wait() + tie().
-template <int RB>
-__device__ __forceinline__ int img_lane(int mb, int lane) {
-  const int gi = lane & 15;
-  return img_off<RB>(8 * (lane >> 4) + (gi >> 2), mb + 4 * (gi & 3));
-}
-template <int RB>
-__device__ __forceinline__ bf16x8 img_frag(const LDS_AS char* img, int loff, int kb) {
-  const s16x4 lo = ds_read_tr16_async(img + loff + kb * RB);
-  const s16x4 hi = ds_read_tr16_async(img + loff + (kb + 4) * RB);
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-// DMA ROWS rows of HD bf16 (from token row0; rows past nvalid zero-filled) into such an image
-template <int HD, int ROWS>
-__device__ __forceinline__ void stage_img(__amdgpu_buffer_rsrc_t rs, long ld, int row0, int nvalid,
-                                          LDS_AS char* lds, int wave, int lane) {
-  constexpr int RB = HD * 2;
-  constexpr int PIECES = ROWS * RB / 1024;
-  static_assert(PIECES % 4 == 0, "whole 1-KB pieces per wave");
-#pragma unroll
-  for (int i = 0; i < PIECES / 4; ++i) {
-    const int p = wave + 4 * i;
-    const int off = p * 1024 + lane * 16;
-    const int r = off / RB;
-    const int pc = (off - r * RB) >> 4;                              // physical 16-B chunk
-    const int c = (((pc >> 1) ^ pair_swz<RB>(r)) << 1) | (pc & 1);  // the logical chunk it holds
-    const uint32_t voff = row0 + r < nvalid ? (uint32_t)(((long)(row0 + r) * ld + c * 8) * 2) : VJ_OOB;
-    dma16(rs, lds + p * 1024, voff);
-  }
-}
-
 // Accumulator registers 8s..8s+7 -> bf16 operand fragment.
 __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
   bf16x8 v;
@@ -374,10 +291,8 @@ constexpr float LOG2E = 1.4426950408889634f;
 // ------------------------------------------------------------------------------------------------
 // Forward: block = 4 waves x 32 queries, KV tiles of 64 keys double-buffered in LDS.
 template <int HD>
-__global__ __launch_bounds__(256, (HD == 64 && VJ_ATTN_FWD_RING ? VJ_ATTN_FWD_RING_OCC : HD == 32 ? VJ_ATTN_FWD32_OCC : HD <= 64 ? VJ_ATTN_FWD_OCC : 2))
-void k_attn_fwd(AttnArgs a) {
+__global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
-  constexpr bool RING = VJ_ATTN_FWD_RING && HD == 64;
   constexpr int KT = 64;
   constexpr int TB = KT * HDP * 2;  // bytes per K or V tile
   __shared__ __attribute__((aligned(16))) char smem_raw[4 * TB];
@@ -435,10 +350,10 @@ void k_attn_fwd(AttnArgs a) {
   stage_rows<HD, KT>(rk, a.ld, 0, len, smem, wave, lane, 4);
   stage_rows<HD, KT>(rv, a.ld, 0, len, smem + TB, wave, lane, 4);
   __syncthreads();
-  // VJ_ATTN_PRIO (head dim 64): s_setprio 1 around the S (bit 0) / PV (bit 1) MFMA clusters, so a
-  // wave's MFMA chain keeps the issue arbitration over the other waves' softmax VALU
-  constexpr bool PRIO_S = HD == 64 && (VJ_ATTN_PRIO & 1);
-  constexpr bool PRIO_PV = HD == 64 && (VJ_ATTN_PRIO & 2);
+  // head dim 64: s_setprio 1 around the S and PV MFMA clusters, so a wave's MFMA chain keeps the
+  // issue arbitration over the other waves' softmax VALU (-2.3 % target, r03_attn_prio_kernels.txt)
+  constexpr bool PRIO_S = HD == 64;
+  constexpr bool PRIO_PV = HD == 64;
   // loop body with the LDS buffer index as a compile-time constant (unrolled by 2), so every LDS
   // address is a per-lane base register plus an immediate offset
   auto tile_iter = [&](const int kt, auto cur_c) {
@@ -448,8 +363,7 @@ void k_attn_fwd(AttnArgs a) {
     if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
       LDS_AS char* nx = smem + (cur ^ 1) * 2 * TB;
       stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
-      // VJ_ATTN_FWD_SPREAD: the V tile after the S MFMAs (under the softmax) instead of in one burst
-      if (!VJ_ATTN_FWD_SPREAD) stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
+      stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
     }
     f32x16 st[2];
 #pragma unroll
@@ -458,28 +372,7 @@ void k_attn_fwd(AttnArgs a) {
       for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
     constexpr int VIMG = cur * 2 * TB + TB;
     bf16x8 vf[4][HDP / 32];
-    if constexpr (RING) {
-      // K fragments in a ring of two k-steps (step s + 1 read under step s's two MFMAs) and only
-      // the first two k-steps of V^T read before the softmax (the other two under the PV MFMAs):
-      // the live registers fit four workgroups per CU
-      bf16x8 kr[2][2];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) kr[0][kk] = row_frag<HDP>(Ks, kk * 32, 0, lane);
-#pragma unroll
-      for (int s = 0; s < HDP / 16; ++s) {
-        if (s + 1 < HDP / 16)
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk) kr[(s + 1) & 1][kk] = row_frag<HDP>(Ks, kk * 32, s + 1, lane);
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kr[s & 1][kk], qf[s], st[kk], 0, 0, 0);
-      }
-#pragma unroll
-      for (int d = 0; d < HDP / 32; ++d) {
-        vf[0][d] = tr_frag_at<HDP, VIMG, 0>(vlo[d], vhi[d]);
-        vf[1][d] = tr_frag_at<HDP, VIMG, 16>(vlo[d], vhi[d]);
-      }
-    } else {
+    {
       // all K fragments first (one LDS wait), then two independent S^T chains interleaved
       bf16x8 kf[2][HDP / 16];
 #pragma unroll
@@ -502,11 +395,6 @@ void k_attn_fwd(AttnArgs a) {
         vf[2][d] = tr_frag_at<HDP, VIMG, 32>(vlo[d], vhi[d]);
         vf[3][d] = tr_frag_at<HDP, VIMG, 48>(vlo[d], vhi[d]);
       }
-    }
-    if (VJ_ATTN_FWD_SPREAD && kt + 1 < nkt) {
-      __builtin_amdgcn_sched_barrier(0);
-      stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, smem + (cur ^ 1) * 2 * TB + TB, wave, lane, 4);
-      __builtin_amdgcn_sched_barrier(0);
     }
     const int kb = kt * KT;
     if (kb + KT > kmask0) {  // ragged last tile (or frame-causal boundary tiles): keys past the limit get -inf
@@ -549,30 +437,7 @@ void k_attn_fwd(AttnArgs a) {
     lsum += ls0 + ls1;
     // O^T += V^T P^T over 4 key-steps of 16
     lds_wait();
-    if constexpr (RING) {
-      tie(vf[0]);
-      tie(vf[1]);
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        if (ks == 2) {  // the last two k-steps' V^T, read under the first two's MFMAs
-          lds_wait();
-          tie(vf[2]);
-          tie(vf[3]);
-        }
-        const bf16x8 pf = acc_frag(st[ks >> 1], ks & 1);
-#pragma unroll
-        for (int d = 0; d < HDP / 32; ++d) ot[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks][d], pf, ot[d], 0, 0, 0);
-        if (ks == VJ_ATTN_FWD_RING_V) {
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int d = 0; d < HDP / 32; ++d) {
-            vf[2][d] = tr_frag_at<HDP, VIMG, 32>(vlo[d], vhi[d]);
-            vf[3][d] = tr_frag_at<HDP, VIMG, 48>(vlo[d], vhi[d]);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    } else {
+    {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) tie(vf[ks]);
       if (PRIO_PV) __builtin_amdgcn_s_setprio(1);
@@ -606,61 +471,23 @@ void k_attn_fwd(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// -delta[h][t] = -sum_d dO[t][h*hd+d] * O[t][h*hd+d]   (one thread per (token, head))
-template <int HD>
-__global__ void k_attn_delta(AttnArgs a) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)a.T * a.H) return;
-  const int t = (int)(i / a.H), h = (int)(i % a.H);
-  const bf16x8* o = (const bf16x8*)(a.o + (long)t * a.ldo + h * HD);
-  const bf16x8* g = (const bf16x8*)(a.dout + (long)t * a.lddo + h * HD);
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < HD / 8; ++k) {
-    const bf16x8 x = o[k], y = g[k];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += (float)x[j] * (float)y[j];
-  }
-  a.stats[(long)a.H * a.T + (long)h * a.T + t] = -s;  // stored negated: the backward's initial dP accumulator
-}
-
-// ------------------------------------------------------------------------------------------------
 // dK/dV: block = 4 waves x (32 KW) keys; sweep query tiles of 32 (Q, dO, lse, delta staged in LDS).
 // Each wave owns KW 32-key tiles (key tile kw of wave w: keys kw*128 + w*32 + 0..31 of the block),
 // so every staged Q / dO fragment feeds KW independent MFMA chains per barrier.
-// DQ (fused dQ, head dims 32 / 64, non-causal): the block's K rows sit in an LDS image; each query
-// tile's dS (bf16, the values the dK product uses) goes to a key-major LDS image, and after the
-// tile's barrier the block computes its dQ partial dQ^T = K^T dS^T over its own keys with 16x16x32
-// MFMAs (wave w: output blocks w, w+4 of the (hd/16) x 2 grid of 16x16 blocks), stored f32 to
-// a.dqp; k_attn_dq_reduce sums the key blocks in a fixed order. No recomputation of S, P, dP.
-// fused dQ product serialised before the S / dP MFMAs instead of interleaved with them (measurement)
-#ifndef VJ_ATTN_DQ_SERIAL
-#define VJ_ATTN_DQ_SERIAL 0
-#endif
-// dK/dV workgroups per CU the register budget is sized for (head dims <= 64); 1 = no bound
-#ifndef VJ_ATTN_DKDV_OCC
-#define VJ_ATTN_DKDV_OCC 1
-#endif
-template <int HD, int KW, bool DQ = false>
-__global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) void k_attn_bwd_dkdv(AttnArgs a) {
+template <int HD, int KW>
+__global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
-  static_assert(!DQ || HD == 32 || HD == 64, "fused dQ: head dims 32 and 64");
   constexpr int QT = 32;
   constexpr int TB = QT * HDP * 2;
   // per stage: Q tile, dO tile, 32 lse + 32 delta floats
   constexpr int STAGE = 2 * TB + 256;
-  constexpr int NK = 128 * KW;               // keys per block
-  constexpr int KIMG = DQ ? NK * HD * 2 : 0;  // K image of the block's keys (fused dQ)
-  constexpr int DSB = DQ ? NK * 64 : 0;       // one dS image: [NK keys][32 queries] bf16
-  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE + KIMG + 2 * DSB];
+  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
-  [[maybe_unused]] LDS_AS char* kimg = smem + 2 * STAGE;
-  [[maybe_unused]] LDS_AS char* dsimg = kimg + KIMG;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tile_id, h;
   xcd_tile(tile_id, h);
-  int seq0, len, kt, grp, sq;
-  locate(a.sg, tile_id, 128 * KW, seq0, len, kt, &grp, &sq);
+  int seq0, len, kt;
+  locate(a.sg, tile_id, 128 * KW, seq0, len, kt);
   int kloc[KW];
   bool kok[KW];
 #pragma unroll
@@ -690,44 +517,6 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
   const __amdgpu_buffer_rsrc_t rs =
       make_rsrc(a.stats + (long)h * a.T + seq0, (uint32_t)min(((long)a.H * a.T + len) * 4, 0x7fffffffL));
   const long dstat = (long)a.H * a.T;  // element distance lse -> delta
-  [[maybe_unused]] long pbase = 0;
-  if constexpr (DQ) {
-    const __amdgpu_buffer_rsrc_t rk = make_rsrc(a.qkv + (long)seq0 * a.ld + a.k_off + h * HD, qbytes);
-    stage_img<HD, NK>(rk, a.ld, kt * NK, len, kimg, wave, lane);  // published by the first barrier
-    const int nkb = (len + NK - 1) / NK;
-    pbase = a.sg.part_off[grp] + ((long)(sq * a.H + h) * nkb + kt) * len * HD;
-  }
-  // fused dQ of query tile `qtile` from the dS image D (all 4 waves' keys: after the tile's barrier)
-  [[maybe_unused]] auto dq_tile = [&](const int qtile, const LDS_AS char* D) {
-    constexpr int NB = HD / 16 * 2;  // 16x16 blocks of dQ^T: hd / 16 row blocks x 2 query halves
-#pragma unroll
-    for (int bi = 0; bi < NB / 4; ++bi) {
-      const int b = wave + 4 * bi;
-      const int m0 = 16 * (b >> 1), n0 = 16 * (b & 1);
-      int le = lane;
-      asm volatile("" : "+v"(le));  // per-call lane addressing (not hoisted to live across the sweep)
-      const int la = img_lane<2 * HD>(m0, le), lb = img_lane<64>(n0, le);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k2 = 0; k2 < NK / 64; ++k2) {  // two 32-key steps per LDS wait
-        bf16x8 fa[2], fb[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          fa[u] = img_frag<2 * HD>(kimg, la, 64 * k2 + 32 * u);
-          fb[u] = img_frag<64>(D, lb, 64 * k2 + 32 * u);
-        }
-        lds_wait();
-        tie(fa);
-        tie(fb);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u], fb[u], acc, 0, 0, 0);
-      }
-      // lane: dQ^T rows m0 + 4(lane>>4) + 0..3 (head dims) of query n0 + (lane&15)
-      const int q = qtile * QT + n0 + (lane & 15);
-      if (q < len) *(f32x4*)(a.dqp + pbase + (long)q * HD + m0 + 4 * (lane >> 4)) = acc;
-    }
-  };
-
   f32x16 dvt[KW][HDP / 32], dkt[KW][HDP / 32];
 #pragma unroll
   for (int kw = 0; kw < KW; ++kw)
@@ -795,67 +584,13 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
         dp[kw][r] = dl;
       }
     }
-    if constexpr (!DQ || VJ_ATTN_DQ_SERIAL) {
-      if constexpr (DQ) {  // the previous query tile's dS (image cur ^ 1, complete since the last barrier)
-        if (qt > qt_first) dq_tile(qt - 1, dsimg + (cur ^ 1) * DSB);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (VJ_ATTN_BPRIO & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int s = 0; s < HDP / 16; ++s)
+    for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
-        for (int kw = 0; kw < KW; ++kw) {
-          sacc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[kw][s], sacc[kw], 0, 0, 0);
-          dp[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[kw][s], dp[kw], 0, 0, 0);
-        }
-      if (VJ_ATTN_BPRIO & 1) __builtin_amdgcn_s_setprio(0);
-    } else {
-      // This tile's S / dP MFMAs interleaved with the previous tile's fused dQ product: dQ chunk c
-      // (two 32-key steps of one 16x16 block) is read from LDS one step ahead, into alternating
-      // fragment registers, and multiplied after the (s, kw) pair c of S / dP, so the transposed-read
-      // latency hides under those MFMAs.
-      constexpr int NSD = HDP / 16 * KW;
-      constexpr int NKC = NK / 64;                  // chunks per 16x16 block
-      constexpr int NCH = (HD / 16 * 2 / 4) * NKC;  // chunks per wave
-      static_assert(NSD == NCH, "one dQ chunk per S / dP MFMA pair");
-      const bool dqp = qt > qt_first;
-      const LDS_AS char* D = dsimg + (cur ^ 1) * DSB;
-      int le = lane;
-      asm volatile("" : "+v"(le));
-      bf16x8 fa[2][2], fb[2][2];
-      f32x4 dacc = {0.f, 0.f, 0.f, 0.f};
-      auto reads = [&](int c, bf16x8 (&xa)[2], bf16x8 (&xb)[2]) {
-        const int b = wave + 4 * (c / NKC), k2 = c % NKC;
-        const int la = img_lane<2 * HD>(16 * (b >> 1), le), lb = img_lane<64>(16 * (b & 1), le);
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          xa[u] = img_frag<2 * HD>(kimg, la, 64 * k2 + 32 * u);
-          xb[u] = img_frag<64>(D, lb, 64 * k2 + 32 * u);
-        }
-      };
-      if (dqp) reads(0, fa[0], fb[0]);
-#pragma unroll
-      for (int c = 0; c < NSD; ++c) {
-        const int s = c / KW, kw = c % KW;
+      for (int kw = 0; kw < KW; ++kw) {
         sacc[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa[s], kf[kw][s], sacc[kw], 0, 0, 0);
         dp[kw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da[s], vf[kw][s], dp[kw], 0, 0, 0);
-        if (dqp) {
-          lds_wait();
-          tie(fa[c & 1]);
-          tie(fb[c & 1]);
-          if (c + 1 < NCH) reads(c + 1, fa[(c + 1) & 1], fb[(c + 1) & 1]);
-#pragma unroll
-          for (int u = 0; u < 2; ++u)
-            dacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[c & 1][u], fb[c & 1][u], dacc, 0, 0, 0);
-          if (c % NKC == NKC - 1) {  // block done: store its partial
-            const int b = wave + 4 * (c / NKC);
-            const int q = (qt - 1) * QT + 16 * (b & 1) + (le & 15);
-            if (q < len) *(f32x4*)(a.dqp + pbase + (long)q * HD + 16 * (b >> 1) + 4 * (le >> 4)) = dacc;
-            dacc = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-        }
       }
-    }
     bf16x8 dtf[2][HDP / 32], qtf[2][HDP / 32];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -883,24 +618,6 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
         sacc[kw][r] = p;
         dp[kw][r] *= p;
       }
-    if constexpr (DQ) {  // dS rows (this lane's key, 4 consecutive queries per 8-B write) into image cur;
-      // keys past the end get 0 (their K rows are zero, but their P can overflow: no inf * 0)
-      LDS_AS char* D = dsimg + cur * DSB + wave * 32 * 64;
-      int le = lane;
-      asm volatile("" : "+v"(le));
-#pragma unroll
-      for (int kw = 0; kw < KW; ++kw) {
-        const int row = kw * 128 + (le & 31);  // + wave * 32 in D (swizzle: row bits 1 and 3 only)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-          const u32x2 v = kok[kw] ? u32x2{pack_bf2(dp[kw][4 * g4], dp[kw][4 * g4 + 1]),
-                                          pack_bf2(dp[kw][4 * g4 + 2], dp[kw][4 * g4 + 3])}
-                                  : u32x2{0u, 0u};
-          *(LDS_AS u32x2*)(D + img_off<64>(row, 8 * g4 + 4 * hl)) = v;
-        }
-      }
-    }
     // dV^T += dO^T P ; dK^T += Q^T dS   (k-permuted accumulators as B operands)
     lds_wait();
 #pragma unroll
@@ -908,7 +625,6 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
       tie(dtf[s2]);
       tie(qtf[s2]);
     }
-    if (VJ_ATTN_BPRIO & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -921,14 +637,12 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
           dkt[kw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtf[s2][d], sf, dkt[kw][d], 0, 0, 0);
         }
       }
-    if (VJ_ATTN_BPRIO & 2) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
   };
   for (int qt0 = qt_first; qt0 < nqt; qt0 += 2) {
     tile_iter(qt0, std::integral_constant<int, 0>{});
     if (qt0 + 1 < nqt) tile_iter(qt0 + 1, std::integral_constant<int, 1>{});
   }
-  if constexpr (DQ) dq_tile(nqt - 1, dsimg + ((nqt - 1 - qt_first) & 1) * DSB);
 #pragma unroll
   for (int kw = 0; kw < KW; ++kw) {
     if (!kok[kw]) continue;
@@ -959,14 +673,10 @@ __global__ __launch_bounds__(256, (DQ ? 2 : HD <= 64 ? VJ_ATTN_DKDV_OCC : 1)) vo
 // dQ: block = 4 waves x (32 QW) queries; sweep key tiles of 64 (K, V staged in LDS). Each wave owns
 // QW 32-query tiles (tile qw of wave w: queries qw*128 + w*32 + 0..31 of the block), so every K / V
 // fragment read from LDS feeds QW independent MFMA chains.
-#ifndef VJ_ATTN_DQ64_OCC  // head dim 64: 3 workgroups per CU at 168 VGPRs (one dword reloaded per key tile): bwd -2..-3 % (bench_kernels)
-#define VJ_ATTN_DQ64_OCC 3
-#endif
-#ifndef VJ_ATTN_DQ_OCC
-#define VJ_ATTN_DQ_OCC 1
-#endif
+// It runs first and computes delta = rowsum(dO * O) itself (from its dO fragments and O), writing
+// -delta to stats for the dK/dV sweep.
 template <int HD, int QW>
-__global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_ATTN_DQ_OCC : 1)) void k_attn_bwd_dq(AttnArgs a) {
+__global__ __launch_bounds__(256, (HD == 64 ? DQ64_OCC : 1)) void k_attn_bwd_dq(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr int KT = 64;
   constexpr int TB = KT * HDP * 2;
@@ -994,7 +704,7 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
       gf[qw][s] = gload8(grow + 16 * s + 8 * hl, qok[qw] && 16 * s + 8 * hl < HD);
     }
     lse2[qw] = qok[qw] ? a.stats[(long)h * a.T + seq0 + qloc[qw]] : 0.f;
-    if (a.dq_delta) {  // -delta = -sum_d dO * O: lanes q and q + 32 hold the two halves of each 16-dim step
+    {  // -delta = -sum_d dO * O: lanes q and q + 32 hold the two halves of each 16-dim step
       const bf16_t* orow = a.o + (long)(seq0 + qloc[qw]) * a.ldo + h * HD;
       float sd = 0.f;
 #pragma unroll
@@ -1006,8 +716,6 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
       sd = sum_xor32(sd);
       dl[qw] = qok[qw] ? -sd : 0.f;
       if (qok[qw] && hl == 0) a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc[qw]] = -sd;
-    } else {
-      dl[qw] = qok[qw] ? a.stats[(long)a.H * a.T + (long)h * a.T + seq0 + qloc[qw]] : 0.f;
     }
   }
 
@@ -1083,7 +791,6 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
           st[qw][r] = nl2[qw];
           dpt[qw][r] = dl[qw];
         }
-      if (VJ_ATTN_BPRIO & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
@@ -1091,7 +798,6 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
           st[qw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka[s], qf[qw][s], st[qw], 0, 0, 0);
           dpt[qw] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va[s], gf[qw][s], dpt[qw], 0, 0, 0);
         }
-      if (VJ_ATTN_BPRIO & 1) __builtin_amdgcn_s_setprio(0);
       // keys past the end are zero rows of K and V; masked on the ragged last tile only so an
       // extreme lse cannot turn 2^(-lse2) * 0 into inf * 0
       if (ragged) {  // uniform branch, last tile only
@@ -1109,7 +815,6 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
       lds_wait();
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) tie(ktf[s2]);
-      if (VJ_ATTN_BPRIO & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -1119,7 +824,6 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
           for (int d = 0; d < HDP / 32; ++d)
             dqt[qw][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktf[s2][d], sf, dqt[qw][d], 0, 0, 0);
         }
-      if (VJ_ATTN_BPRIO & 2) __builtin_amdgcn_s_setprio(0);
     }
     __syncthreads();
   };
@@ -1146,50 +850,6 @@ __global__ __launch_bounds__(256, (HD == 64 ? VJ_ATTN_DQ64_OCC : HD <= 64 ? VJ_A
         if (col < HD) *(uint32_t*)(dq + col) = pack_bf2(dqt[qw][d][r], dqt[qw][d][r + 1]);
       }
   }
-}
-
-// Inverse RoPE of one (d, d + 1) pair of a row (the scalar form of rope_inv_rows)
-template <int HD>
-__device__ __forceinline__ void rope_inv_pair(const AttnArgs& a, const TokPos& tp, int d, float& x0, float& x1) {
-  constexpr int half = (HD / 3) / 2, sw = 2 * half;
-  if (d >= 3 * sw) return;
-  const int ax = d / sw, js = d - ax * sw;
-  const int pos = (ax == 0 ? tp.fr : (ax == 1 ? tp.hr : tp.wc)) * half;
-  const int i0 = pos + js % half, i1 = pos + (js + 1) % half;
-  const float c0 = a.cos_t[i0], s0 = a.sin_t[i0], c1 = a.cos_t[i1], s1 = a.sin_t[i1];
-  const float y0 = x0 * c0 + x1 * s1, y1 = -x0 * s0 + x1 * c1;
-  x0 = y0;
-  x1 = y1;
-}
-
-// Fused backward, second pass: dQ = scale * (sum over the key blocks of the dQ partials, in block
-// order), inverse RoPE, bf16 into the q columns of dqkv. One thread per (token, head, 4 head dims).
-template <int HD, int NK>
-__global__ void k_attn_dq_reduce(AttnArgs a) {
-  constexpr int G = HD / 4;
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)a.T * a.H * G) return;
-  const int dg = (int)(i % G);
-  const long th = i / G;
-  const int h = (int)(th % a.H), t = (int)(th / a.H);
-  int g = 0;
-#pragma unroll
-  for (int j = 1; j < MAXG; ++j)
-    if (j < a.sg.ngroups && t >= a.sg.tok0[j]) g = j;
-  const int len = a.sg.len[g], loc = t - a.sg.tok0[g];
-  const int s = loc / len, q = loc - s * len;
-  const int nkb = (len + NK - 1) / NK;
-  const float* p = a.dqp + a.sg.part_off[g] + (long)(s * a.H + h) * nkb * len * HD + (long)q * HD + 4 * dg;
-  f32x4 acc = *(const f32x4*)p;
-  for (int kb = 1; kb < nkb; ++kb) acc += *(const f32x4*)(p + (long)kb * len * HD);
-  float x[4] = {acc[0] * a.scale, acc[1] * a.scale, acc[2] * a.scale, acc[3] * a.scale};
-  if (a.cos_t) {
-    const TokPos tp = tok_pos(a, t);
-    rope_inv_pair<HD>(a, tp, 4 * dg, x[0], x[1]);
-    rope_inv_pair<HD>(a, tp, 4 * dg + 2, x[2], x[3]);
-  }
-  *(uint2*)(a.dqkv + (long)t * a.ldd + a.q_off + h * HD + 4 * dg) =
-      make_uint2(pack_bf2(x[0], x[1]), pack_bf2(x[2], x[3]));
 }
 
 int fill_groups(SeqGroups& sg, int ngroups, const int* nseq, const int* len, int tile, long T) {
@@ -1259,58 +919,12 @@ extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q
                         stream);
 }
 
-// keys per block of the fused backward (0: no fused kernel for this head dim)
-static int fused_nk(int hd) { return hd == 32 ? 128 * VJ_ATTN_KW32 : hd == 64 ? 128 * VJ_ATTN_KW64 : 0; }
-
-// fused-backward dQ partials: sum over groups of nseq * H * ceil(len / NK) * len * hd floats
-static long part_elems(int H, int hd, int ngroups, const int* nseq, const int* len, long* off) {
-  const int nk = fused_nk(hd);
-  long tot = 0;
-  for (int g = 0; g < MAXG; ++g) {
-    if (off) off[g] = tot;
-    if (g < ngroups && nk) tot += (long)nseq[g] * H * ((len[g] + nk - 1) / nk) * (long)len[g] * hd;
-  }
-  return tot;
-}
-
-extern "C" int vj_attn_bwd_ws_bytes(int H, int hd, int ngroups, const int* nseq, const int* len, long* bytes) {
-  VJ_CHECK_ARG(bytes && nseq && len && ngroups >= 1 && ngroups <= MAXG, "vj_attn_bwd_ws_bytes: bad arguments");
-  *bytes = 4 * part_elems(H, hd, ngroups, nseq, len, nullptr);
-  return VJ_OK;
-}
-
-static int attn_bwd_impl(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
-                         const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
-                         float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
-                         int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t, int fblk,
-                         void* ws, long ws_bytes, void* stream);
 
 extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
                               const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
                               long ldd, float scale, int ngroups, const int* nseq, const int* len,
                               const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t,
                               const float* sin_t, int fblk, void* stream) {
-  return attn_bwd_impl(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
-                       nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, fblk, nullptr, 0, stream);
-}
-
-// As vj_attn_bwd_fc with a workspace of vj_attn_bwd_ws_bytes: head dims 32 / 64 without a frame-causal
-// mask then run the fused backward (dQ partials per key block from the dK/dV sweep + a reduce pass)
-// instead of a separate dQ sweep; other layouts, or a NULL / short workspace, take the two sweeps.
-extern "C" int vj_attn_bwd_ws(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
-                              const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
-                              long ldd, float scale, int ngroups, const int* nseq, const int* len,
-                              const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t,
-                              const float* sin_t, int fblk, void* ws, long ws_bytes, void* stream) {
-  return attn_bwd_impl(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
-                       nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, fblk, ws, ws_bytes, stream);
-}
-
-static int attn_bwd_impl(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
-                         const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd,
-                         float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
-                         int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t, int fblk,
-                         void* ws, long ws_bytes, void* stream) {
   if (T == 0) return VJ_OK;
   int rc = check_common(H, hd, ld, ldo);
   if (rc) return rc;
@@ -1330,61 +944,30 @@ static int attn_bwd_impl(int T, int H, int hd, const void* qkv, long ld, int q_o
   a.o = (bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.stats = stats;
   a.dqkv = (bf16_t*)dqkv; a.ldd = ldd; a.H = H; a.T = T; a.scale = scale; a.fblk = fblk;
   // key / query 32-row tiles per wave of the two sweeps (block tile = 128 x that)
-  const int kw = hd == 32 ? VJ_ATTN_KW32 : hd == 64 ? VJ_ATTN_KW64 : 1;
-  const int qw = hd == 32 ? VJ_ATTN_QW32 : hd == 64 ? VJ_ATTN_QW64 : 1;
+  const int kw = hd == 32 ? KW32 : hd == 64 ? KW64 : 1;
+  const int qw = hd == 32 ? QW32 : hd == 64 ? QW64 : 1;
   AttnArgs ak = a, aq = a;
   rc = fill_groups(ak.sg, ngroups, nseq, len, 128 * kw, T);
   if (rc) return rc;
   rc = fill_groups(aq.sg, ngroups, nseq, len, 128 * qw, T);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  const long nth = (long)T * H;
-  const int dblocks = (int)((nth + 255) / 256);
   const dim3 gk(ak.sg.tiles_prefix[MAXG], H), gq(aq.sg.tiles_prefix[MAXG], H);
-  // fused backward, opt-in (VJ_ATTN_FUSED=1): delta, dK/dV + dQ partials, dQ reduce. Measured slower
-  // than the two sweeps (attention backward), so the default stays the two sweeps.
-  const char* fenv = getenv("VJ_ATTN_FUSED");
-  const bool fused = ws && fblk == 0 && fused_nk(hd) > 0 && fenv && fenv[0] == '1' &&
-                     ws_bytes >= 4 * part_elems(H, hd, ngroups, nseq, len, nullptr) && ((uintptr_t)ws & 15) == 0;
-  if (fused) {
-    ak.dqp = (float*)ws;
-    part_elems(H, hd, ngroups, nseq, len, ak.sg.part_off);
-    const long nr = (long)T * H * (hd / 4);
-    const dim3 gr((unsigned)((nr + 255) / 256));
-    if (hd == 64) {
-      hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64, true>), gk, dim3(256), 0, st, ak);
-      hipLaunchKernelGGL((k_attn_dq_reduce<64, 128 * VJ_ATTN_KW64>), gr, dim3(256), 0, st, ak);
-    } else {
-      hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32, true>), gk, dim3(256), 0, st, ak);
-      hipLaunchKernelGGL((k_attn_dq_reduce<32, 128 * VJ_ATTN_KW32>), gr, dim3(256), 0, st, ak);
-    }
-    VJ_LAUNCH_CHECK("vj_attn_bwd");
-    return VJ_OK;
-  }
-  // dQ sweep first: it writes -delta for the dK/dV sweep (VJ_ATTN_DELTA=1: the separate delta kernel)
-  const char* denv = getenv("VJ_ATTN_DELTA");
-  const bool sep = denv && denv[0] == '1';
-  aq.dq_delta = sep ? 0 : 1;
+  // dQ sweep first: it writes -delta for the dK/dV sweep
   switch (hd) {
     case 64:
-      if (sep) hipLaunchKernelGGL(k_attn_delta<64>, dim3(dblocks), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((k_attn_bwd_dq<64, VJ_ATTN_QW64>), gq, dim3(256), 0, st, aq);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<64, VJ_ATTN_KW64>), gk, dim3(256), 0, st, ak);
+      hipLaunchKernelGGL((k_attn_bwd_dq<64, QW64>), gq, dim3(256), 0, st, aq);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<64, KW64>), gk, dim3(256), 0, st, ak);
       break;
     case 32:
-      if (sep) hipLaunchKernelGGL(k_attn_delta<32>, dim3(dblocks), dim3(256), 0, st, a);
-      hipLaunchKernelGGL((k_attn_bwd_dq<32, VJ_ATTN_QW32>), gq, dim3(256), 0, st, aq);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<32, VJ_ATTN_KW32>), gk, dim3(256), 0, st, ak);
+      hipLaunchKernelGGL((k_attn_bwd_dq<32, QW32>), gq, dim3(256), 0, st, aq);
+      hipLaunchKernelGGL((k_attn_bwd_dkdv<32, KW32>), gk, dim3(256), 0, st, ak);
       break;
     case 80:
-      if (sep) hipLaunchKernelGGL(k_attn_delta<80>, dim3(dblocks), dim3(256), 0, st, a);
       hipLaunchKernelGGL((k_attn_bwd_dq<80, 1>), gq, dim3(256), 0, st, aq);
       hipLaunchKernelGGL((k_attn_bwd_dkdv<80, 1>), gk, dim3(256), 0, st, ak);
       break;
     default:
-      if (sep) hipLaunchKernelGGL(k_attn_delta<88>, dim3(dblocks), dim3(256), 0, st, a);
       hipLaunchKernelGGL((k_attn_bwd_dq<88, 1>), gq, dim3(256), 0, st, aq);
       hipLaunchKernelGGL((k_attn_bwd_dkdv<88, 1>), gk, dim3(256), 0, st, ak);
       break;

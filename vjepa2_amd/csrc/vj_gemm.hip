@@ -257,15 +257,6 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
                         int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
                         void* C2, long ldc2, hipStream_t st, const void* rope);
 
-static int use_gemm256() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("VJ_GEMM256");
-    v = (e && e[0] == '0') ? 0 : 1;
-  }
-  return v;
-}
-
 extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B,
                                    long ldb, int b_kmajor, int epi, const float* bias, const void* aux, long ldaux,
                                    void* C, long ldc, void* C2, long ldc2, int splitk, float* ws, long ws_floats,
@@ -303,18 +294,16 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
   dim3 grid(vj_cdiv(N, BN), vj_cdiv(M, BM), splitk);
   VJ_CHECK_ARG(grid.y <= 65535, "vj_gemm_bf16: M too large");
   hipStream_t st = (hipStream_t)stream;
-#ifndef VJ_GEMM256_MINK
-#define VJ_GEMM256_MINK 0
-#endif
-  if (splitk == 1 && M >= 1024 && N >= 128 && K >= VJ_GEMM256_MINK && use_gemm256()) {
+  // the 256-row persistent kernel (vj_gemm256.hip) where it takes the shape; this file's 128 x 128
+  // kernel for the rest (small M / N, layouts it declines)
+  if (splitk == 1 && M >= 1024 && N >= 128) {
     const int rc = vj_gemm256_dispatch(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, epi, bias, aux, ldaux, C, ldc, C2,
                                        ldc2, st, nullptr);
     if (rc != VJ_ERR_UNSUPPORTED) return rc;
   }
   if (splitk > 1) {
     int rc = VJ_ERR_UNSUPPORTED;
-    if (use_gemm256())
-      rc = vj_gemm256_partial(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, kslice, splitk, ws, st);
+    rc = vj_gemm256_partial(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, kslice, splitk, ws, st);
     if (rc == VJ_ERR_UNSUPPORTED) {
       if (a_kmajor && b_kmajor) rc = launch_epi<true, true>(EPI_PARTIAL, g, grid, st);
       else if (a_kmajor && !b_kmajor) rc = launch_epi<true, false>(EPI_PARTIAL, g, grid, st);

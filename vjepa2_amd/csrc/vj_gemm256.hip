@@ -1129,8 +1129,7 @@ extern "C" int vj_qkv_rope_gemm(int M, int K, const void* A, long lda, const voi
   VJ_CHECK_ARG(hd % 8 == 0 && cos_t && sin_t && (ids || ids_mod > 0), "vj_qkv_rope_gemm: bad rope arguments");
   VJ_CHECK_ARG(tpf > 0 && tpr > 0 && npos > 0, "vj_qkv_rope_gemm: tokens_per_frame/row and npos must be > 0");
   const int half = (hd / 3) / 2;
-  const char* e = getenv("VJ_GEMM256");
-  if (M >= 1024 && !(e && e[0] == '0')) {
+  if (M >= 1024) {
     RopeP rp{ids, ids_mod, tpf, tpr, half, hd, H * hd, cos_t, sin_t, npos};
     const int rc = vj_gemm256_dispatch(M, N, K, A, lda, 1, B, ldb, 1, EPI_ROPE, bias, nullptr, 0, C, ldc, nullptr, 0,
                                        (hipStream_t)stream, &rp);

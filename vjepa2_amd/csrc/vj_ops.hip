@@ -1150,8 +1150,8 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
   }
   hipStream_t st = (hipStream_t)stream;
   float* part = nsum ? ws : nullptr;
-  const char* e = getenv("VJ_LN_V1");
-  const bool v2 = !(e && e[0] == '1') && D % 8 == 0 && lddy % 8 == 0 && ldx % 4 == 0 && ldr % 4 == 0 &&
+  // k_ln_bwd2 (16-B accesses); k_ln_bwd for strides that do not allow 16-B vectors
+  const bool v2 = D % 8 == 0 && lddy % 8 == 0 && ldx % 4 == 0 && ldr % 4 == 0 &&
                   (!dres_in || ldri % 4 == 0) && (!dres_bf16 || ldrb % 8 == 0) && D <= 2048;
   int nbl = nb;  // blocks launched (<= nb: the workspace sizing of vj_layernorm_bwd_blocks)
   if (v2) {  // 16-B accesses (8 columns per lane-vector); a grid every CU holds at once (3 blocks)

@@ -408,18 +408,10 @@ def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None, fblk
     dqkv = dqkv if dqkv is not None else torch.empty(T, 3 * D, dtype=BF16, device=qkv.device)
     ns, ln = [g[0] for g in groups], [g[1] for g in groups]
     ids, mod, tpf, tpr, ct, st = rope if rope is not None else (None, 0, 0, 0, None, None)
-    ws = None
-    if fblk == 0 and hd in (32, 64) and os.environ.get("VJ_ATTN_FUSED") == "1":
-        # opt-in fused backward: dQ partials per key block (f32 workspace); measured slower, DESIGN.md
-        import ctypes
-
-        nbytes = ctypes.c_long(0)
-        call("vj_attn_bwd_ws_bytes", H, hd, len(groups), int_array(ns), int_array(ln), ctypes.byref(nbytes))
-        ws = torch.empty(max(4, nbytes.value // 4), dtype=F32, device=qkv.device)
-    _call("vj_attn_bwd_ws", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
+    _call("vj_attn_bwd_fc", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
           _rowmajor(do, "do"), _p(stats), _p(dqkv), _rowmajor(dqkv, "dqkv"), float(scale), len(groups), int_array(ns),
-          int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), int(fblk), _p(ws),
-          0 if ws is None else ws.numel() * 4, _stream(), label=f"attn_bwd<hd{hd}>",
+          int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), int(fblk), _stream(),
+          label=f"attn_bwd<hd{hd}>",
           flops=sum(10.0 * n * l * l * D for n, l in groups))  # FA2 convention: 5 matmuls = 2.5 x forward
     return dqkv
 

@@ -578,12 +578,15 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // ~36k cycles per tile vs ~10k without the reads, but deeper prefetch (3, 5, 7) measured no
       // faster: the 64 MB of residual every CU reads at once is the bound, not the latency chain
       [[maybe_unused]] float aux[AUX_PF + 1][4][NTN];
+      // per-tile lane offsets (elements): row r of virtual m-tile i is then + (rowoff(i) + r) * ld, a
+      // wave-uniform (scalar) product, instead of a 64-bit multiply per row
+      [[maybe_unused]] const long off_aux = AUX ? (long)mb * g.ldaux + nb : 0;
       auto fetch = [&](int i, float (&dst)[4][NTN]) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = mb + rowoff(i) + r;
           const bool ok = m < g.M && nok;
-          const long off = ok ? (long)m * g.ldaux + nb : 0;
+          const long off = ok ? off_aux + (long)(rowoff(i) + r) * g.ldaux : 0;
           if constexpr (EPI == EPI_F32_RESID) {
             if constexpr (NTN == 4) {
               const float4 x = *(const float4*)((const float*)g.aux + off);
@@ -611,23 +614,35 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       const bool odd = lane & 1;
       const int nb8 = nb - (odd ? 4 : 0);
       const bool nok8 = nb8 < g.N;
-      auto store_wide = [&](bf16_t* base, long ld, int i, const uint32_t (&pk)[4][2]) {
-        uint32_t snd[4], rcv[4];
+      const int mrow = mb + (odd ? 2 : 0);  // first row this lane stores of a virtual m-tile
+      // every register index below is a compile-time constant (a lane-dependent row index into pk
+      // compiled to a compare / select chain over all 8 words per store)
+      auto store_wide = [&](bf16_t* base, long ld, long off, int i, const uint32_t (&pk)[4][2]) {
+        uint32_t snd[4], keep[4], rcv[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) snd[k] = odd ? pk[k >> 1][k & 1] : pk[2 + (k >> 1)][k & 1];
+        for (int k = 0; k < 4; ++k) {
+          snd[k] = odd ? pk[k >> 1][k & 1] : pk[2 + (k >> 1)][k & 1];
+          keep[k] = odd ? pk[2 + (k >> 1)][k & 1] : pk[k >> 1][k & 1];
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) rcv[k] = dpp_u<DPP_XOR1>(snd[k]);  // lane pair exchange on the VALU
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int r = odd ? 2 + h : h;
-          const int m = mb + rowoff(i) + r;
-          if (m < g.M && nok8) {
-            const uint4 v = odd ? make_uint4(rcv[2 * h], rcv[2 * h + 1], pk[r][0], pk[r][1])
-                                : make_uint4(pk[r][0], pk[r][1], rcv[2 * h], rcv[2 * h + 1]);
-            *(uint4*)(base + (long)m * ld + nb8) = v;
+          if (mrow + rowoff(i) + h < g.M && nok8) {
+            const uint32_t a = 2 * h, b = 2 * h + 1;
+            const uint4 v = make_uint4(odd ? rcv[a] : keep[a], odd ? rcv[b] : keep[b], odd ? keep[a] : rcv[a],
+                                       odd ? keep[b] : rcv[b]);
+            *(uint4*)(base + off + (long)(rowoff(i) + h) * ld) = v;
           }
         }
       };
+      // per-tile lane offsets of the bf16 outputs (C, C2) and the f32 output rows
+      [[maybe_unused]] const long off_c = (long)mrow * g.ldc + nb8;
+      [[maybe_unused]] const long off_c2 = EPI == EPI_GELU ? (long)mrow * g.ldc2 + nb8 : 0;
+      [[maybe_unused]] const long off_f = EPI == EPI_PARTIAL ? ((long)cur.z * g.M + mb) * g.N + nb
+                                                             : (long)mb * g.ldc + nb;
+      [[maybe_unused]] const long ld_f = EPI == EPI_PARTIAL ? (long)g.N : g.ldc;
+      [[maybe_unused]] float* const base_f = EPI == EPI_PARTIAL ? g.ws : (float*)g.C;
       if constexpr (AUX)
 #pragma unroll
         for (int i = 0; i < AUX_PF; ++i) fetch(i, aux[i]);
@@ -671,8 +686,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           for (int r = 0; r < 4; ++r) {
             const int m = mb + rowoff(i) + r;
             if (m < g.M && nok) {
-              float* dst = EPI == EPI_PARTIAL ? g.ws + ((long)cur.z * g.M + m) * g.N + nb
-                                              : (float*)g.C + (long)m * g.ldc + nb;
+              float* dst = base_f + off_f + (long)(rowoff(i) + r) * ld_f;
               if constexpr (M32)
                 *(f32x4*)dst = f32x4{accv(i, r, 0), accv(i, r, 1), accv(i, r, 2), accv(i, r, 3)};
               else
@@ -706,8 +720,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           }
           if constexpr (F32OUT) {
             if (m < g.M && nok) {
-              float* dst = EPI == EPI_PARTIAL ? g.ws + ((long)cur.z * g.M + m) * g.N + nb
-                                              : (float*)g.C + (long)m * g.ldc + nb;
+              float* dst = base_f + off_f + (long)(rowoff(i) + r) * ld_f;
               *(float4*)dst = make_float4(v[0], v[1], v[2], v[3]);
             }
           } else {
@@ -724,8 +737,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           }
         }
         if constexpr (!F32OUT) {
-          if (EPI != EPI_GELU || SAVE_D) store_wide((bf16_t*)g.C, g.ldc, i, pk);
-          if constexpr (EPI == EPI_GELU) store_wide((bf16_t*)g.C2, g.ldc2, i, ga);
+          if (EPI != EPI_GELU || SAVE_D) store_wide((bf16_t*)g.C, g.ldc, off_c, i, pk);
+          if constexpr (EPI == EPI_GELU) store_wide((bf16_t*)g.C2, g.ldc2, off_c2, i, ga);
         }
       }
       };

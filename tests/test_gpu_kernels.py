@@ -713,6 +713,64 @@ def test_gemm_mfma32_matches_mfma16(K, pxcd, monkeypatch):
         _close(m32["gelu_bwd"], (X.float() @ W.float().t()) * dgs.float(), 2e-3, 1.5e-2, "mfma32 EPI_GELU_BWD")
 
 
+@pytest.mark.parametrize("K", [32, 64, 96, 384, 1024])
+@pytest.mark.parametrize("pxcd", [None, "1", "3"])
+def test_gemm_staggered_matches_one_tile(K, pxcd, monkeypatch):
+    """The staggered main loop (VJ_GEMM_STG=1: 32-deep K units in a 4-slot LDS ring, one stream of
+    units across the block's tiles, waves 4-7 one barrier behind waves 0-3) runs the same MFMAs on
+    every accumulator in the same K order as the one-tile kernel, so every epilogue's output is
+    bitwise equal. K = 32 / 64 / 96 make 1 / 2 / 3 units per tile (the DMA stream runs 2 units ahead,
+    i.e. up to 2 tiles ahead), VJ_GEMM_PXCD = 1 / 3 give many tiles per block (epilogue / tile
+    hand-over paths of both wave halves), M = 2100 / 1333 ragged last row tiles, N = 1000 a ragged
+    last column tile; plus the fused QKV + RoPE epilogue."""
+    from vjepa2_amd import ops
+
+    if pxcd:
+        monkeypatch.setenv("VJ_GEMM_PXCD", pxcd)
+    monkeypatch.setenv("VJ_GEMM_BM192", "0")  # 256-row tiles for both
+    g = torch.Generator(device="cpu").manual_seed(K + 7)
+    for M, N in [(2100, 512), (1333, 1000)]:
+        X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+        W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
+        b = torch.randn(N, generator=g).to(DEV)
+        resid = torch.randn(M, N, generator=g).to(DEV)
+        dgs = torch.randn(M, N, generator=g).to(DEV).bfloat16()
+
+        def run():
+            outs = {"bf16": ops.linear_fwd(X, W, b, ops.EPI_BF16),
+                    "f32": ops.linear_fwd(X, W, b, ops.EPI_F32),
+                    "f32_resid": ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid),
+                    "bf16_resid": ops.linear_fwd(X, W, b, ops.EPI_BF16_RESID, resid=resid.bfloat16())}
+            d, a = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
+            outs["gelu_d"], outs["gelu_a"] = d, a
+            outs["gelu_nosave"] = ops.linear_fwd(X, W, b, ops.EPI_GELU)[1]
+            gb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(M, N, K, X, K, True, W, K, True, ops.EPI_GELU_BWD, out=gb, ldc=N, aux=dgs, ldaux=N)
+            outs["gelu_bwd"] = gb
+            torch.cuda.synchronize()
+            return {k: v.detach().clone() for k, v in outs.items()}
+
+        monkeypatch.setenv("VJ_GEMM_STG", "0")
+        one = run()
+        monkeypatch.setenv("VJ_GEMM_STG", "1")
+        stg = run()
+        for k in one:
+            assert torch.equal(stg[k], one[k]), f"staggered {k} != one-tile kernel (M={M} N={N} K={K} pxcd={pxcd})"
+    # QKV GEMM with the fused RoPE epilogue (N = 3 * 4 * 64 = 768: 256-wide tiles)
+    H, hd, M = 4, 64, 2100
+    ids = torch.randint(0, 8 * 16, (M,), generator=g).to(DEV).int()
+    cos_t, sin_t = (t.to(DEV) for t in orc.rope_tables(hd, 16))
+    x = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    w = (0.1 * torch.randn(3 * H * hd, K, generator=g)).to(DEV).bfloat16()
+    bq = torch.randn(3 * H * hd, generator=g).to(DEV)
+    res = []
+    for stg in ("0", "1"):
+        monkeypatch.setenv("VJ_GEMM_STG", stg)
+        res.append(ops.qkv_rope(x, w, bq, H, hd, ids, 0, 16, 4, cos_t, sin_t).clone())
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1]), f"staggered qkv_rope != one-tile kernel (K={K} pxcd={pxcd})"
+
+
 @pytest.mark.parametrize("K", [64, 128, 1024])
 @pytest.mark.parametrize("pxcd", [None, "1"])
 def test_gemm_192_row_tiles_match_256(K, pxcd, monkeypatch):

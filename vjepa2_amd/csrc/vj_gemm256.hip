@@ -40,6 +40,9 @@
 //  * one m-tile of residual / saved-derivative rows prefetched ahead in the direct epilogue (deeper:
 //    no faster, r03 stamps).
 constexpr int SPLIT_AT = 3;
+#ifndef VJ_STG_PRIO  // experiment build: s_setprio 1 around the staggered loop's MFMA intervals
+#define VJ_STG_PRIO 0
+#endif
 constexpr int DMA_WAVES = 4;
 constexpr int AUX_PF = 1;
 
@@ -56,8 +59,11 @@ __device__ long vj_gemm_stamps[2048 * 16 * 4];
 // BMT = 192 (8-wave, K-major bf16, 256-wide direct-store tiles only): 96-row wave tiles (3 m-tiles
 // per M-half) for problems whose 256-row tile count leaves a round of CUs under-filled (context
 // GEMMs, M ~ 11.7k: 184 tiles of 256 x 256 on 256 CUs -> 244 tiles of 192 x 256).
-template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, bool M32 = false>
+template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, bool M32 = false,
+          bool STG = false>
 __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
+  static_assert(!STG || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256 && !M32 && EPI != EPI_PARTIAL),
+                "staggered main loop: 8-wave K-major bf16 256 x 256 tiles");
   static_assert(!F8 || (AK && BKM && EPI != EPI_PARTIAL && EPI != EPI_GELU_BWD), "fp8: forward GEMMs only");
   static_assert(NWV == 8 || (NWV == 4 && AK && BKM && !F8), "2-workgroup GEMM: K-major bf16 operands only");
   static_assert(!M32 || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256),
@@ -190,8 +196,69 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   int wg = run0 + jb;
   Tile cur = make_tile(wg);
   int par = 0;  // LDS slot of K-tile t of the current tile: (t + par) & 1
-  load_tile(cur, 0, 0, lane);
-  if (cur.nk > 1) load_tile(cur, 1, 1, lane);
+
+  // ---- STG: staggered main loop (GEMM). 32-deep K units in a ring of 4 LDS slots (A
+  // 256 x 32 then B 256 x 32, 16 KB each); the block's tiles form ONE stream of units (position q =
+  // unit q % nku of the block's tile q / nku), and position q + 2 is DMA'd while q is computed, so the
+  // next tile's first units arrive under this tile's last ones and its epilogue. Each wave issues 4
+  // of the 32 1-KB pieces of every unit (waves 0-3: A, 4-7: B; their lane offsets are fixed per
+  // tile, the unit's K offset rides in soffset), 2 per load interval; past the stream end the pieces
+  // zero-fill an unread slot, so the per-wave vmcnt count stays 4.
+  constexpr int USZ = 32768;
+  [[maybe_unused]] const int nku = STG ? (g.K + 31) / 32 : 0;
+  [[maybe_unused]] int dwg = wg, dku = 0, dpos = 0;
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t drs;
+  [[maybe_unused]] uint32_t dvo[4];
+  const bool isA = wave < 4;
+  auto dma_setup = [&]() {  // lane offsets / descriptor of this wave's operand of DMA tile dwg
+    if (dwg < runend) {
+      const Tile T = make_tile(dwg);
+      const int left = isA ? g.M - T.m0 : g.N - T.n0;
+      const long ld = isA ? g.lda : g.ldb;
+      if (isA) drs = make_rsrc(g.A + (long)T.m0 * g.lda, clampb((long)left * g.lda * 2));
+      else drs = make_rsrc(g.B + (long)T.n0 * g.ldb, clampb((long)left * g.ldb * 2));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = (4 * (wave & 3) + j) * 16 + (lane >> 2);  // LDS row of the lane's 16-B chunk
+        const int c = (lane & 3) ^ ((r >> 2) & 3);              // its logical chunk (64-B row swizzle)
+        int gr = r;
+        if (!isA) {  // PERM (stage()): LDS row r of a 64-row group holds group row 4 (r % 16) + r / 16
+          const int rl = r & 63;
+          gr = (r - rl) + 4 * (rl & 15) + (rl >> 4);
+        }
+        dvo[j] = gr < left ? (uint32_t)(gr * ld * 2 + c * 16) : VJ_OOB;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dvo[j] = VJ_OOB;
+    }
+  };
+  // this wave's pieces 2h, 2h + 1 of stream position dpos (into slot dpos & 3)
+  auto dma_half = [&](auto h_c) {
+    constexpr int h = decltype(h_c)::value;
+    LDS_AS char* dst = smem + (dpos & 3) * USZ + (isA ? 0 : 16384) + (4 * (wave & 3) + 2 * h) * 1024;
+    const int soff = __builtin_amdgcn_readfirstlane(dku * 64);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst, 16, dvo[2 * h], soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst + 1024, 16, dvo[2 * h + 1], soff, 0, 0);
+    if constexpr (h == 1) {
+      ++dpos;
+      if (++dku == nku) {
+        dku = 0;
+        dwg += P;
+        dma_setup();
+      }
+    }
+  };
+  if constexpr (STG) {
+    dma_setup();
+    dma_half(std::integral_constant<int, 0>{});
+    dma_half(std::integral_constant<int, 1>{});
+    dma_half(std::integral_constant<int, 0>{});
+    dma_half(std::integral_constant<int, 1>{});
+  } else {
+    load_tile(cur, 0, 0, lane);
+    if (cur.nk > 1) load_tile(cur, 1, 1, lane);
+  }
   if constexpr (EPI == EPI_ROPE) {
 #pragma unroll
     for (int i = 0; i < RTR; ++i) {
@@ -356,176 +423,258 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         f8sb[j] = 127 + (n < g.N ? g.eb[n] : 0);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if constexpr (F8) {
-      rdA8(Xa, par, 0);
-      rdB8(0, NTN / 2, par);
-    } else if constexpr (M32) {
-      rd32(Aa, Ba, par, 0);
-    } else {
-      rdA(Aa, par, 0, 0);
-      rdB(Ba, par, 0);
+    // STG: the bias columns are loaded before the main loop (in the epilogue the load would wait for
+    // the next tile's DMA pieces issued after it: vmcnt counts in order)
+    [[maybe_unused]] float biasp[NTN];
+    if constexpr (STG) {
+      const int nbp = cur.n0 + wc * WN + NTN * (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NTN; ++j) biasp[j] = 0.f;
+      if (EPI != EPI_GELU_BWD && g.bias && nbp < g.N)
+#pragma unroll
+        for (int j = 0; j < NTN; ++j) biasp[j] = g.bias[nbp + j];
     }
-
-    // Per K-tile t: 4 phases, each with the fragments of the NEXT phase read while the current
-    // phase's MFMAs run: 16x16x32 (k-step, M-half) = (0,0) (0,1) (1,0) (1,1), 4*NTN MFMAs each;
-    // 32x32x16 k-steps 0..3, 8 MFMAs each. One barrier per tile, before phase 3 (whose prefetch reads
-    // tile t+1): it retires this wave's DMA of tile t+1 (issued one tile earlier) and its reads of
-    // tile t; then slot (t + par) & 1 is free for the DMA of tile t+2, or of the next tile's stages
-    // once this tile has none left.
-    const __amdgpu_buffer_rsrc_t ra = rsrc_a(cur), rb = rsrc_b(cur);
-    // 8-wave bf16 main loop: only the A pieces of K-tile t + 2 go out after the barrier; the B pieces
-    // are issued inside the last phase's MFMAs (SPLIT: m-tiles / MFMAs before them)
-    constexpr bool SPREAD = NWV == 8 && !F8 && BK == 64;
-    constexpr int SPLIT = M32 ? 6 : (MH == 4 ? SPLIT_AT : MH - 1);
-    // one K-tile; TAIL (the last two K-tiles) DMAs the next tile's stages instead of this tile's
-    auto ktile = [&](const int t, auto tail_c) {
-      constexpr bool TAIL = decltype(tail_c)::value;
-      const int sl = (t + par) & 1;
-      if constexpr (F8) {
-        // m-quarters q0..q2 (A: Aa, Ab alternate); B's upper n-tiles of this K-tile arrive under
-        // q0's lower-half MFMAs
-        rdB8(NTN / 2, NTN, sl);
-        rdA8(Xb, sl, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm8(Xa, 0, 0, NTN / 2);
-        mm8(Xa, 0, NTN / 2, NTN);
-        __builtin_amdgcn_sched_barrier(0);
-        rdA8(Xa, sl, 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mm8(Xb, 1, 0, NTN);
-        __builtin_amdgcn_sched_barrier(0);
-        rdA8(Xb, sl, 3);
-        __builtin_amdgcn_sched_barrier(0);
-        mm8(Xa, 2, 0, NTN);
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (M32) {
-        // k-steps 0..2 (fragments alternate between (Aa, Ba) and (Ab, Bb))
-        rd32(Ab, Bb, sl, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm32(Aa, Ba, 0, 8);
-        __builtin_amdgcn_sched_barrier(0);
-        rd32(Aa, Ba, sl, 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mm32(Ab, Bb, 0, 8);
-        __builtin_amdgcn_sched_barrier(0);
-        rd32(Ab, Bb, sl, 3);
-        __builtin_amdgcn_sched_barrier(0);
-        mm32(Aa, Ba, 0, 8);
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (BK == 32) {
-        // one k-step: phase 0 = (M-half 0) under the read of M-half 1's A fragments; phase 1 after
-        // the barrier, the next K-tile's fragments read under its MFMAs
-        rdA(Ab, sl, 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(Aa, 0, Ba);
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        release(Aa, Ba);
-        rdA(Ab, sl, 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(Aa, 0, Ba);
-        __builtin_amdgcn_sched_barrier(0);
-        release(Ab, Ba);
-        rdA(Aa, sl, 0, 1);
-        rdB(Bb, sl, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(Ab, 1, Ba);
-        __builtin_amdgcn_sched_barrier(0);
-        release(Aa, Bb);
-        rdA(Ab, sl, 1, 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm(Aa, 0, Bb);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next tile's stage 0 stays in flight
-      if constexpr (ASYNC) {
-        tie(Ab);
-        tie(Bb);
-      }
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!TAIL) {
-        if constexpr (SPREAD) {
-          if (iss)
-            stage<AK, BM, false, DMAW, BK, WNX, PB>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff,
-                                                     smem + sl * STAGE, wave, lane);
-        } else {
-          load_k(ra, rb, cur, t + 2, sl, lane);
+    // STG with a residual / saved-derivative epilogue: the first m-tile of aux rows is fetched one
+    // unit before the tile ends (after that unit's DMA wait), so the epilogue's first reads do not
+    // wait behind the next tile's DMA pieces
+    [[maybe_unused]] f32x4 auxr[AUX && STG ? 4 : 1];
+    auto stg_aux = [&] {
+      if constexpr (AUX && STG) {
+        const int m = cur.m0 + wr * WM + 4 * (lane >> 4);
+        const int n = cur.n0 + wc * WN + NTN * (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = m + r < g.M && n < g.N;
+          const long off = ok ? (long)(m + r) * g.ldaux + n : 0;
+          if constexpr (EPI == EPI_F32_RESID) {
+            auxr[r] = *(const f32x4*)((const float*)g.aux + off);
+          } else {
+            const uint2 x = *(const uint2*)((const bf16_t*)g.aux + off);
+            auxr[r] = f32x4{__builtin_bit_cast(float, x.x), __builtin_bit_cast(float, x.y), 0.f, 0.f};
+          }
         }
-      } else if (has_next) {
-        // slot sl is free: the next tile's stage 0 (t == nk-2) or stage 1 (t == nk-1; stage 0 goes
-        // to the other, unused slot when nk == 1); stage 1 waits for the epilogue unless EARLY1
-        int lt = lane;
-        asm volatile("" : "+v"(lt));  // tail-only addressing: not hoisted across the main loop
-        const Tile nx = make_tile(wgn);
-        if (t + 2 == nk) {
-          load_tile(nx, 0, sl, lt);
-        } else {
-          if (nk == 1) load_tile(nx, 0, sl ^ 1, lt);
-          if (EARLY1 && nx.nk > 1) load_tile8(nx, 1, sl, lt);
-        }
-      }
-      auto b_pieces = [&] {
-        if (iss)
-          stage<BKM, BN, DIRECT, DMAW, BK, WNX, PB>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
-                                                     smem + sl * STAGE + A_BYTES, wave, lane);
-      };
-      if constexpr (F8) {
-        // q3; the next K-tile's q0 A fragments and lower B n-tiles are read under it
-        if (t + 1 < nk) rdA8(Xa, sl ^ 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        mm8(Xb, 3, 0, NTN / 2);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < nk) rdB8(0, NTN / 2, sl ^ 1);
-        __builtin_amdgcn_sched_barrier(0);
-        mm8(Xb, 3, NTN / 2, NTN);
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (M32) {
-        // k-step 3; the next K-tile's k-step 0 fragments are read under it
-        if (t + 1 < nk) rd32(Aa, Ba, sl ^ 1, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (SPREAD && !TAIL) {
-          mm32(Ab, Bb, 0, SPLIT);
-          __builtin_amdgcn_sched_barrier(0);
-          b_pieces();
-          __builtin_amdgcn_sched_barrier(0);
-          mm32(Ab, Bb, SPLIT, 8);
-        } else {
-          mm32(Ab, Bb, 0, 8);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      } else if constexpr (BK == 32) {
-        mm(Ab, 1, Ba);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 1 < nk) {  // overwrite Aa / Ba once phase 1's MFMAs have been issued
-          rdA(Aa, sl ^ 1, 0, 0);
-          rdB(Ba, sl ^ 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      } else {
-        if (t + 1 < nk) {
-          rdA(Aa, sl ^ 1, 0, 0);
-          rdB(Ba, sl ^ 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (SPREAD && !TAIL) {
-          mm_rows(Ab, 1, Bb, 0, SPLIT);
-          __builtin_amdgcn_sched_barrier(0);
-          b_pieces();
-          __builtin_amdgcn_sched_barrier(0);
-          mm_rows(Ab, 1, Bb, SPLIT, MH);
-        } else {
-          mm(Ab, 1, Bb);
-        }
-        __builtin_amdgcn_sched_barrier(0);
       }
     };
-    int t = 0;
-    for (; t + 2 < nk; ++t) ktile(t, std::false_type{});
-    for (; t < nk; ++t) ktile(t, std::true_type{});
+    if constexpr (STG) {
+      // Staggered main loop. Per unit, each wave runs L | M (intervals between workgroup
+      // barriers): L = the unit's fragment reads (A m-tiles 0-7, B n-tiles 0-3: 12 ds_read_b128) + its
+      // 4 DMA pieces of unit q + 2, M = the unit's 32 MFMAs. Waves 4-7 run one interval behind waves
+      // 0-3 (one extra barrier before their first tile), so while one wave of a SIMD pair issues
+      // MFMAs the other reads LDS / issues DMA. Every wave waits for its own pieces of unit q + 1 at
+      // the end of L of unit q (vmcnt(4): the 4 pieces of unit q + 2 stay in flight); the barrier
+      // after it orders them before any wave's reads of q + 1.
+      // Tile boundary: waves 0-3 go from the last M1's barrier into the epilogue and on to the next
+      // tile's L0; waves 4-7 skip that barrier (their epilogue starts right after the last MFMAs)
+      // and take it after the epilogue, before the next tile's L0 - the pairing (and the
+      // half-interval stagger) is unchanged and the two epilogues overlap.
+      if (wg == run0 + jb) {  // first tile: unit 0 landed everywhere, RoPE table published
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (wr == 1) __builtin_amdgcn_s_barrier();
+      }
+      const int q0 = dpos - 2;  // stream position of this tile's unit 0
+      auto bar = [] {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      for (int u = 0; u < nku; ++u) {
+        const LDS_AS char* sA = smem + ((q0 + u) & 3) * USZ;
+        const LDS_AS char* sB = sA + 16384;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Aa[i] = frag<true, 256, 32>(sA, wr * 128 + i * 16, 0, lane);
+#pragma unroll
+        for (int j = 0; j < NTN; ++j) Ba[j] = frag<true, 256, 32>(sB, wc * WN + j * 16, 0, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ab[i] = frag<true, 256, 32>(sA, wr * 128 + 64 + i * 16, 0, lane);
+        dma_half(std::integral_constant<int, 0>{});
+        dma_half(std::integral_constant<int, 1>{});
+        if (AUX && u == nku - 1 && nku > 1) {
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // the aux rows (fetched one unit ago) stay in flight
+        } else {
+          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
+        if (AUX && u == nku - 2) stg_aux();
+        if (AUX && nku == 1) stg_aux();
+        bar();
+        if (VJ_STG_PRIO) __builtin_amdgcn_s_setprio(1);
+        mm(Aa, 0, Ba);
+        mm(Ab, 1, Ba);
+        if (VJ_STG_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (u + 1 < nku || wr == 0) bar();
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if constexpr (F8) {
+        rdA8(Xa, par, 0);
+        rdB8(0, NTN / 2, par);
+      } else if constexpr (M32) {
+        rd32(Aa, Ba, par, 0);
+      } else {
+        rdA(Aa, par, 0, 0);
+        rdB(Ba, par, 0);
+      }
+
+      // Per K-tile t: 4 phases, each with the fragments of the NEXT phase read while the current
+      // phase's MFMAs run: 16x16x32 (k-step, M-half) = (0,0) (0,1) (1,0) (1,1), 4*NTN MFMAs each;
+      // 32x32x16 k-steps 0..3, 8 MFMAs each. One barrier per tile, before phase 3 (whose prefetch reads
+      // tile t+1): it retires this wave's DMA of tile t+1 (issued one tile earlier) and its reads of
+      // tile t; then slot (t + par) & 1 is free for the DMA of tile t+2, or of the next tile's stages
+      // once this tile has none left.
+      const __amdgpu_buffer_rsrc_t ra = rsrc_a(cur), rb = rsrc_b(cur);
+      // 8-wave bf16 main loop: only the A pieces of K-tile t + 2 go out after the barrier; the B pieces
+      // are issued inside the last phase's MFMAs (SPLIT: m-tiles / MFMAs before them)
+      constexpr bool SPREAD = NWV == 8 && !F8 && BK == 64;
+      constexpr int SPLIT = M32 ? 6 : (MH == 4 ? SPLIT_AT : MH - 1);
+      // one K-tile; TAIL (the last two K-tiles) DMAs the next tile's stages instead of this tile's
+      auto ktile = [&](const int t, auto tail_c) {
+        constexpr bool TAIL = decltype(tail_c)::value;
+        const int sl = (t + par) & 1;
+        if constexpr (F8) {
+          // m-quarters q0..q2 (A: Aa, Ab alternate); B's upper n-tiles of this K-tile arrive under
+          // q0's lower-half MFMAs
+          rdB8(NTN / 2, NTN, sl);
+          rdA8(Xb, sl, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          mm8(Xa, 0, 0, NTN / 2);
+          mm8(Xa, 0, NTN / 2, NTN);
+          __builtin_amdgcn_sched_barrier(0);
+          rdA8(Xa, sl, 2);
+          __builtin_amdgcn_sched_barrier(0);
+          mm8(Xb, 1, 0, NTN);
+          __builtin_amdgcn_sched_barrier(0);
+          rdA8(Xb, sl, 3);
+          __builtin_amdgcn_sched_barrier(0);
+          mm8(Xa, 2, 0, NTN);
+          __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (M32) {
+          // k-steps 0..2 (fragments alternate between (Aa, Ba) and (Ab, Bb))
+          rd32(Ab, Bb, sl, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          mm32(Aa, Ba, 0, 8);
+          __builtin_amdgcn_sched_barrier(0);
+          rd32(Aa, Ba, sl, 2);
+          __builtin_amdgcn_sched_barrier(0);
+          mm32(Ab, Bb, 0, 8);
+          __builtin_amdgcn_sched_barrier(0);
+          rd32(Ab, Bb, sl, 3);
+          __builtin_amdgcn_sched_barrier(0);
+          mm32(Aa, Ba, 0, 8);
+          __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (BK == 32) {
+          // one k-step: phase 0 = (M-half 0) under the read of M-half 1's A fragments; phase 1 after
+          // the barrier, the next K-tile's fragments read under its MFMAs
+          rdA(Ab, sl, 1, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          mm(Aa, 0, Ba);
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          release(Aa, Ba);
+          rdA(Ab, sl, 1, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          mm(Aa, 0, Ba);
+          __builtin_amdgcn_sched_barrier(0);
+          release(Ab, Ba);
+          rdA(Aa, sl, 0, 1);
+          rdB(Bb, sl, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          mm(Ab, 1, Ba);
+          __builtin_amdgcn_sched_barrier(0);
+          release(Aa, Bb);
+          rdA(Ab, sl, 1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+          mm(Aa, 0, Bb);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (t + 1 < nk) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next tile's stage 0 stays in flight
+        if constexpr (ASYNC) {
+          tie(Ab);
+          tie(Bb);
+        }
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!TAIL) {
+          if constexpr (SPREAD) {
+            if (iss)
+              stage<AK, BM, false, DMAW, BK, WNX, PB>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff,
+                                                       smem + sl * STAGE, wave, lane);
+          } else {
+            load_k(ra, rb, cur, t + 2, sl, lane);
+          }
+        } else if (has_next) {
+          // slot sl is free: the next tile's stage 0 (t == nk-2) or stage 1 (t == nk-1; stage 0 goes
+          // to the other, unused slot when nk == 1); stage 1 waits for the epilogue unless EARLY1
+          int lt = lane;
+          asm volatile("" : "+v"(lt));  // tail-only addressing: not hoisted across the main loop
+          const Tile nx = make_tile(wgn);
+          if (t + 2 == nk) {
+            load_tile(nx, 0, sl, lt);
+          } else {
+            if (nk == 1) load_tile(nx, 0, sl ^ 1, lt);
+            if (EARLY1 && nx.nk > 1) load_tile8(nx, 1, sl, lt);
+          }
+        }
+        auto b_pieces = [&] {
+          if (iss)
+            stage<BKM, BN, DIRECT, DMAW, BK, WNX, PB>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
+                                                       smem + sl * STAGE + A_BYTES, wave, lane);
+        };
+        if constexpr (F8) {
+          // q3; the next K-tile's q0 A fragments and lower B n-tiles are read under it
+          if (t + 1 < nk) rdA8(Xa, sl ^ 1, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          mm8(Xb, 3, 0, NTN / 2);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + 1 < nk) rdB8(0, NTN / 2, sl ^ 1);
+          __builtin_amdgcn_sched_barrier(0);
+          mm8(Xb, 3, NTN / 2, NTN);
+          __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (M32) {
+          // k-step 3; the next K-tile's k-step 0 fragments are read under it
+          if (t + 1 < nk) rd32(Aa, Ba, sl ^ 1, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (SPREAD && !TAIL) {
+            mm32(Ab, Bb, 0, SPLIT);
+            __builtin_amdgcn_sched_barrier(0);
+            b_pieces();
+            __builtin_amdgcn_sched_barrier(0);
+            mm32(Ab, Bb, SPLIT, 8);
+          } else {
+            mm32(Ab, Bb, 0, 8);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        } else if constexpr (BK == 32) {
+          mm(Ab, 1, Ba);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + 1 < nk) {  // overwrite Aa / Ba once phase 1's MFMAs have been issued
+            rdA(Aa, sl ^ 1, 0, 0);
+            rdB(Ba, sl ^ 1, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        } else {
+          if (t + 1 < nk) {
+            rdA(Aa, sl ^ 1, 0, 0);
+            rdB(Ba, sl ^ 1, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (SPREAD && !TAIL) {
+            mm_rows(Ab, 1, Bb, 0, SPLIT);
+            __builtin_amdgcn_sched_barrier(0);
+            b_pieces();
+            __builtin_amdgcn_sched_barrier(0);
+            mm_rows(Ab, 1, Bb, SPLIT, MH);
+          } else {
+            mm(Ab, 1, Bb);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      int t = 0;
+      for (; t + 2 < nk; ++t) ktile(t, std::false_type{});
+      for (; t < nk; ++t) ktile(t, std::true_type{});
+    }
 
     // the epilogue's lane-derived addressing is recomputed per tile (an opaque copy of the lane id
     // keeps the compiler from hoisting it out of the tile loop, where it would hold VGPRs across the
@@ -547,8 +696,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       const int mb = cur.m0 + wr * WM + lrow;
       float bias[NTN];
 #pragma unroll
-      for (int j = 0; j < NTN; ++j) bias[j] = 0.f;
-      if (EPI != EPI_GELU_BWD && EPI != EPI_PARTIAL && g.bias && nok)
+      for (int j = 0; j < NTN; ++j) bias[j] = STG ? biasp[j] : 0.f;
+      if (!STG && EPI != EPI_GELU_BWD && EPI != EPI_PARTIAL && g.bias && nok)
 #pragma unroll
         for (int j = 0; j < NTN; ++j) bias[j] = g.bias[nb + j];
       // RoPE (modules.py:26-50, 343-365): tile rows' (frame, row, col) positions + interleaved
@@ -645,7 +794,25 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       [[maybe_unused]] float* const base_f = EPI == EPI_PARTIAL ? g.ws : (float*)g.C;
       if constexpr (AUX)
 #pragma unroll
-        for (int i = 0; i < AUX_PF; ++i) fetch(i, aux[i]);
+        for (int i = 0; i < AUX_PF; ++i) {
+          if constexpr (STG) {  // m-tile 0, fetched under the last unit
+            static_assert(AUX_PF == 1, "STG prefetches one m-tile of aux rows");
+            auto lo = [](float u) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, u) << 16); };
+            auto hi = [](float u) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, u) & 0xffff0000u); };
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              if constexpr (EPI == EPI_F32_RESID) {
+#pragma unroll
+                for (int j = 0; j < NTN; ++j) aux[0][r][j] = auxr[r][j];
+              } else {
+                aux[0][r][0] = lo(auxr[r][0]); aux[0][r][1] = hi(auxr[r][0]);
+                aux[0][r][2] = lo(auxr[r][1]); aux[0][r][3] = hi(auxr[r][1]);
+              }
+            }
+          } else {
+            fetch(i, aux[i]);
+          }
+        }
       // GELU: the derivative pass is compiled separately, for callers that save it (g.C)
       auto rows = [&](auto save_c) {
       constexpr bool SAVE_D = decltype(save_c)::value;
@@ -653,7 +820,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       for (int i = 0; i < 2 * MH; ++i) {
         if constexpr (AUX) {
           if (i + AUX_PF < 2 * MH) fetch(i + AUX_PF, aux[(i + AUX_PF) % (AUX_PF + 1)]);
-          if (i == 2 * MH - 1 - AUX_PF && has_next) {  // behind the last aux fetch
+          if (!STG && i == 2 * MH - 1 - AUX_PF && has_next) {  // behind the last aux fetch
             const Tile nxt = make_tile(wgn);
             if (nxt.nk > 1) load_tile8(nxt, 1, sle, lane);
           }
@@ -874,6 +1041,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       ++stamp_it;
     }
 #endif
+    if constexpr (STG) {
+      // waves 4-7: the barrier skipped after their last MFMAs (see the main loop); waves 0-3: the
+      // matching one after the block's last tile, so both halves end with equal barrier counts
+      if (wr == 1 || !has_next) __builtin_amdgcn_s_barrier();
+    }
     if (!has_next) break;
     wg = wgn;
     cur = make_tile(wgn);
@@ -1033,6 +1205,34 @@ bool use_m32(int epi) {
   return false;
 }
 
+// Staggered main loop (STG) for the K-major 256 x 256-tile GEMMs with K % 32 == 0. VJ_GEMM_STG: 0 = never,
+// 1 = always (where the shape takes 256-row tiles), unset = the measured default (GEMM).
+bool use_stg(int K) {
+  if (K % 32) return false;
+  const char* e = getenv("VJ_GEMM_STG");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return false;
+}
+
+int launch_stg(int epi, const G256& g, hipStream_t st) {
+  const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
+#define LSTG(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 256, false, true>), grid, dim3(512), 0, st, g); break
+  switch (epi) {
+    case EPI_BF16: LSTG(EPI_BF16);
+    case EPI_F32: LSTG(EPI_F32);
+    case EPI_F32_RESID: LSTG(EPI_F32_RESID);
+    case EPI_GELU: LSTG(EPI_GELU);
+    case EPI_GELU_BWD: LSTG(EPI_GELU_BWD);
+    case EPI_ROPE: LSTG(EPI_ROPE);
+    case EPI_BF16_RESID: LSTG(EPI_BF16_RESID);
+    default: vj_set_error("gemm256(stg): bad epilogue %d", epi); return VJ_ERR_ARG;
+  }
+#undef LSTG
+  VJ_LAUNCH_CHECK("vj_gemm256(stg)");
+  return VJ_OK;
+}
+
 template <bool AK, bool BKM, int BN>
 int launch256(int epi, const G256& g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n * g.nsplit));
@@ -1098,6 +1298,7 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
       return launch192(epi, g, st);
     }
     if (a_kmajor && b_kmajor && use_m32(epi)) return launch32(epi, g, st);
+    if (a_kmajor && b_kmajor && use_stg(K)) return launch_stg(epi, g, st);
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
     if (a_kmajor && !b_kmajor) return launch256<true, false, 256>(epi, g, st);
     if (!a_kmajor && b_kmajor) return launch256<false, true, 256>(epi, g, st);

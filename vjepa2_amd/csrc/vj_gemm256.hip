@@ -100,7 +100,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // it) or issues global loads that would queue behind the DMA in vmcnt order (AUX: once the last
   // aux rows are fetched).
   constexpr bool EARLY1 = DIRECT && !AUX;
-  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE + TAB_BYTES];
+  // STG: ring of NSL 32-KB unit slots, DMA distance NSL - 2 units; 5 slots (all 160 KB of the CU's
+  // LDS, distance 3) unless the RoPE epilogue needs the table area (4 slots + table, distance 2)
+  constexpr int NSL = STG ? (EPI == EPI_ROPE ? 4 : 5) : 1;
+  constexpr int DIST = NSL - 2;
+  __shared__ __attribute__((aligned(16))) char smem_raw[STG && NSL == 5 ? 5 * 32768 : 2 * STAGE + TAB_BYTES];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   LDS_AS char* tab = smem + 2 * STAGE;
 
@@ -233,10 +237,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       for (int j = 0; j < 4; ++j) dvo[j] = VJ_OOB;
     }
   };
-  // this wave's pieces 2h, 2h + 1 of stream position dpos (into slot dpos & 3)
+  // this wave's pieces 2h, 2h + 1 of stream position dpos (into slot dpos % NSL)
   auto dma_half = [&](auto h_c) {
     constexpr int h = decltype(h_c)::value;
-    LDS_AS char* dst = smem + (dpos & 3) * USZ + (isA ? 0 : 16384) + (4 * (wave & 3) + 2 * h) * 1024;
+    LDS_AS char* dst = smem + (dpos % NSL) * USZ + (isA ? 0 : 16384) + (4 * (wave & 3) + 2 * h) * 1024;
     const int soff = __builtin_amdgcn_readfirstlane(dku * 64);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst, 16, dvo[2 * h], soff, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst + 1024, 16, dvo[2 * h + 1], soff, 0, 0);
@@ -251,10 +255,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   };
   if constexpr (STG) {
     dma_setup();
-    dma_half(std::integral_constant<int, 0>{});
-    dma_half(std::integral_constant<int, 1>{});
-    dma_half(std::integral_constant<int, 0>{});
-    dma_half(std::integral_constant<int, 1>{});
+#pragma unroll
+    for (int i = 0; i < DIST; ++i) {
+      dma_half(std::integral_constant<int, 0>{});
+      dma_half(std::integral_constant<int, 1>{});
+    }
   } else {
     load_tile(cur, 0, 0, lane);
     if (cur.nk > 1) load_tile(cur, 1, 1, lane);
@@ -425,14 +430,17 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     }
     // STG: the bias columns are loaded before the main loop (in the epilogue the load would wait for
     // the next tile's DMA pieces issued after it: vmcnt counts in order)
+    // (loads issued between the DMA pieces only ever make the main loop's counted vmcnt waits wait
+    // longer, never shorter: its counts assume the DMA pieces alone)
     [[maybe_unused]] float biasp[NTN];
     if constexpr (STG) {
       const int nbp = cur.n0 + wc * WN + NTN * (lane & 15);
 #pragma unroll
       for (int j = 0; j < NTN; ++j) biasp[j] = 0.f;
-      if (EPI != EPI_GELU_BWD && g.bias && nbp < g.N)
-#pragma unroll
-        for (int j = 0; j < NTN; ++j) biasp[j] = g.bias[nbp + j];
+      if (EPI != EPI_GELU_BWD && g.bias && nbp < g.N) {
+        const float4 bv = *(const float4*)(g.bias + nbp);
+        biasp[0] = bv.x; biasp[1] = bv.y; biasp[2] = bv.z; biasp[3] = bv.w;
+      }
     }
     // STG with a residual / saved-derivative epilogue: the first m-tile of aux rows is fetched one
     // unit before the tile ends (after that unit's DMA wait), so the epilogue's first reads do not
@@ -468,18 +476,19 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // and take it after the epilogue, before the next tile's L0 - the pairing (and the
       // half-interval stagger) is unchanged and the two epilogues overlap.
       if (wg == run0 + jb) {  // first tile: unit 0 landed everywhere, RoPE table published
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        if constexpr (DIST == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         if (wr == 1) __builtin_amdgcn_s_barrier();
       }
-      const int q0 = dpos - 2;  // stream position of this tile's unit 0
+      const int q0 = dpos - DIST;  // stream position of this tile's unit 0
       auto bar = [] {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       };
       for (int u = 0; u < nku; ++u) {
-        const LDS_AS char* sA = smem + ((q0 + u) & 3) * USZ;
+        const LDS_AS char* sA = smem + ((q0 + u) % NSL) * USZ;
         const LDS_AS char* sB = sA + 16384;
 #pragma unroll
         for (int i = 0; i < 4; ++i) Aa[i] = frag<true, 256, 32>(sA, wr * 128 + i * 16, 0, lane);
@@ -489,10 +498,16 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         for (int i = 0; i < 4; ++i) Ab[i] = frag<true, 256, 32>(sA, wr * 128 + 64 + i * 16, 0, lane);
         dma_half(std::integral_constant<int, 0>{});
         dma_half(std::integral_constant<int, 1>{});
+        // unit q + 1 landed: the pieces of units q + 2 .. q + DIST (4 each) stay in flight, and the aux
+        // rows fetched one unit ago
+        // rows fetched one unit ago (exactly 4 loads per lane: one per row). Any other load issued
+        // after unit q + 1's pieces (the tile's bias / RoPE ids) only lengthens the wait.
         if (AUX && u == nku - 1 && nku > 1) {
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // the aux rows (fetched one unit ago) stay in flight
+          if constexpr (DIST == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else {
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          if constexpr (DIST == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         }
         if (AUX && u == nku - 2) stg_aux();
         if (AUX && nku == 1) stg_aux();
@@ -1206,13 +1221,16 @@ bool use_m32(int epi) {
 }
 
 // Staggered main loop (STG) for the K-major 256 x 256-tile GEMMs with K % 32 == 0. VJ_GEMM_STG: 0 = never,
-// 1 = always (where the shape takes 256-row tiles), unset = the measured default (GEMM).
-bool use_stg(int K) {
+// 1 = always (where the shape takes 256-row tiles), unset = the measured default: the epilogues that
+// read no aux rows (GELU, RoPE, bf16 / f32 out). Measured in the train step (rocprofv3, one call,
+// profiles/r04_gemm_staggered_step.txt): GELU -1.8 %, RoPE -1.6 %, bf16 -1.7 %, but the residual /
+// saved-derivative epilogues +1..+4 % (bf16 residual, K = 4096 target fc2: +4 %).
+bool use_stg(int K, int epi) {
   if (K % 32) return false;
   const char* e = getenv("VJ_GEMM_STG");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return false;
+  return epi == EPI_GELU || epi == EPI_ROPE || epi == EPI_BF16 || epi == EPI_F32;
 }
 
 int launch_stg(int epi, const G256& g, hipStream_t st) {
@@ -1298,7 +1316,7 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
       return launch192(epi, g, st);
     }
     if (a_kmajor && b_kmajor && use_m32(epi)) return launch32(epi, g, st);
-    if (a_kmajor && b_kmajor && use_stg(K)) return launch_stg(epi, g, st);
+    if (a_kmajor && b_kmajor && use_stg(K, epi)) return launch_stg(epi, g, st);
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
     if (a_kmajor && !b_kmajor) return launch256<true, false, 256>(epi, g, st);
     if (!a_kmajor && b_kmajor) return launch256<false, true, 256>(epi, g, st);

@@ -1090,13 +1090,16 @@ extern "C" int vj_layernorm_fwd(int M, int D, const void* x, int x_bf16, long ld
   VJ_CHECK_ARG((gamma == nullptr) == (beta == nullptr), "vj_layernorm_fwd: gamma/beta both or neither");
   VJ_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "vj_layernorm_fwd: strides must be %%4");
   hipStream_t st = (hipStream_t)stream;
-  // k_ln_fwd3 (all rows of a wave in flight, 16-B accesses) where the row fits its register budget and
-  // the strides allow 16-B vectors; else the one-row-lookahead k_ln_fwd. VJ_LN_FWD=1 forces k_ln_fwd
-  // (A/B). (Round 3's persistent 16-B variant k_ln_fwd2 measured slower than k_ln_fwd and was removed.)
+  // k_ln_fwd3 (all rows of a wave in flight, 16-B accesses) for bf16 inputs where the row fits its
+  // register budget and the strides allow 16-B vectors; else the one-row-lookahead k_ln_fwd.
+  // Measured (profiles/r04_ln_fwd_kernels.txt): bf16 target rows 42.3 -> 37.6 us, but f32 rows (the
+  // training path's residual stream) 18.0 -> 20.4 / 27.9 -> 31.2 us, so f32 inputs keep k_ln_fwd.
+  // VJ_LN_FWD=1 forces k_ln_fwd, 3 forces k_ln_fwd3 where it applies (A/B). (Round 3's persistent
+  // 16-B variant k_ln_fwd2 measured slower than k_ln_fwd and was removed.)
   const int E = x_bf16 ? 8 : 4;
   const int nv3 = (D + 64 * E - 1) / (64 * E);
   const char* e = getenv("VJ_LN_FWD");
-  const bool v3 = !(e && e[0] == '1') && D % E == 0 && ldx % E == 0 && ldy % (y_f32 ? 4 : E) == 0 && nv3 <= 4 &&
+  const bool v3 = !(e && e[0] == '1') && (x_bf16 || (e && e[0] == '3')) && D % E == 0 && ldx % E == 0 && ldy % (y_f32 ? 4 : E) == 0 && nv3 <= 4 &&
                   !((uintptr_t)x & 15) && !((uintptr_t)y & 15) && !((uintptr_t)gamma & 15) && !((uintptr_t)beta & 15);
   if (v3) {
     constexpr int R = 4;

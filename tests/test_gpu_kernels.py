@@ -417,19 +417,15 @@ def test_fused_rope_paths(M, hd, H, monkeypatch):
     b = torch.randn(3 * D, generator=g).to(DEV)
     fused = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
     if M >= 1024:
-        monkeypatch.setenv("VJ_GEMM_MF", "16")
-        f16 = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
-        for bm in ("1", "0"):  # 192-row tiles (where N takes 256-wide ones) == 256-row tiles, bitwise
+        # 192-row tiles (where N takes 256-wide ones), the one-tile and the staggered main loop: the
+        # same MFMAs in the same K order, bitwise equal
+        for bm, stg in (("1", "0"), ("0", "0"), ("0", "1")):
             monkeypatch.setenv("VJ_GEMM_BM192", bm)
+            monkeypatch.setenv("VJ_GEMM_STG", stg)
             other = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
-            assert torch.equal(f16, other), f"qkv_rope: VJ_GEMM_BM192={bm} differs from the 16x16x32 kernel"
+            assert torch.equal(fused, other), f"qkv_rope: VJ_GEMM_BM192={bm} VJ_GEMM_STG={stg} differs"
         monkeypatch.delenv("VJ_GEMM_BM192")
-        # 32x32x16 form (256-wide tiles only): another K order inside each MFMA, one bf16 rounding apart
-        monkeypatch.setenv("VJ_GEMM_MF", "32")
-        f32x = ops.qkv_rope(x, w, b, H, hd, ids, 0, tpf, tpr, cos_t, sin_t)
-        monkeypatch.delenv("VJ_GEMM_MF")
-        _close(f32x, f16, 1e-3, 8e-3, "qkv_rope 32x32x16 vs 16x16x32")
-        assert torch.equal(fused, f16) or torch.equal(fused, f32x), "default kernel is neither MFMA form"
+        monkeypatch.delenv("VJ_GEMM_STG")
     # expected: our own f32 GEMM (same accumulation), RoPE in fp32 by the oracle
     y32 = ops.linear_fwd(x, w, b, ops.EPI_F32).cpu()
     idl = ids.cpu().long()[None]
@@ -657,18 +653,17 @@ def test_adamw_ema_fused_equals_separate(skip):
 
 @pytest.mark.parametrize("K", [64, 192, 256, 1024])
 @pytest.mark.parametrize("pxcd", [None, "1", "3"])
-def test_gemm_mfma32_matches_mfma16(K, pxcd, monkeypatch):
-    """The 32x32x16 form of the 256 x 256-tile kernel (VJ_GEMM_MF=32: waves 4 x 2, wave tile 64 x 128,
-    B staged with a 32-row permutation) against the 16x16x32 form (VJ_GEMM_MF=16) on every epilogue:
-    another K summation order inside each MFMA, so f32 outputs agree to accumulation rounding and bf16
-    outputs to one rounding step (few of them differ at all); both against fp32 math. K = 64 / 192 /
-    256 make 1 / 3 / 4 K-tiles (tail paths), VJ_GEMM_PXCD = 1 / 3 many tiles per block (the next
-    tile's stages DMA'd under the epilogue), M = 2100 / 1333 ragged last row tiles and N = 1000 a
-    ragged last column tile."""
+def test_gemm_256_tiles_vs_fp32(K, pxcd, monkeypatch):
+    """The 256 x 256-tile kernel (one-tile main loop: VJ_GEMM_STG=0, 256-row tiles) on every epilogue
+    against fp32 math: K = 64 / 192 / 256 make 1 / 3 / 4 K-tiles (tail paths), VJ_GEMM_PXCD = 1 / 3
+    many tiles per block (the next tile's stages DMA'd under the epilogue), M = 2100 / 1333 ragged
+    last row tiles and N = 1000 a ragged last column tile."""
     from vjepa2_amd import ops
 
     if pxcd:
         monkeypatch.setenv("VJ_GEMM_PXCD", pxcd)
+    monkeypatch.setenv("VJ_GEMM_BM192", "0")
+    monkeypatch.setenv("VJ_GEMM_STG", "0")
     g = torch.Generator(device="cpu").manual_seed(K)
     for M, N in [(2100, 512), (1333, 1000)]:
         X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
@@ -677,40 +672,21 @@ def test_gemm_mfma32_matches_mfma16(K, pxcd, monkeypatch):
         resid = torch.randn(M, N, generator=g).to(DEV)
         dgs = torch.randn(M, N, generator=g).to(DEV).bfloat16()
         ref = X.float() @ W.float().t() + b
-
-        def run():
-            outs = {"bf16": ops.linear_fwd(X, W, b, ops.EPI_BF16),
-                    "f32": ops.linear_fwd(X, W, b, ops.EPI_F32),
-                    "f32_resid": ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid),
-                    "bf16_resid": ops.linear_fwd(X, W, b, ops.EPI_BF16_RESID, resid=resid.bfloat16())}
-            d, a = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
-            outs["gelu_d"], outs["gelu_a"] = d, a
-            outs["gelu_nosave"] = ops.linear_fwd(X, W, b, ops.EPI_GELU)[1]
-            gb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-            ops.gemm(M, N, K, X, K, True, W, K, True, ops.EPI_GELU_BWD, out=gb, ldc=N, aux=dgs, ldaux=N)
-            outs["gelu_bwd"] = gb
-            torch.cuda.synchronize()
-            return {k: v.detach().clone() for k, v in outs.items()}
-
-        monkeypatch.setenv("VJ_GEMM_BM192", "0")  # 256-row tiles for both forms
-        monkeypatch.setenv("VJ_GEMM_MF", "16")
-        m16 = run()
-        monkeypatch.setenv("VJ_GEMM_MF", "32")
-        m32 = run()
-        monkeypatch.delenv("VJ_GEMM_MF")
-        monkeypatch.delenv("VJ_GEMM_BM192")
-        tol32 = 2e-6 * math.sqrt(K) * float(ref.abs().max())
-        for k in ("f32", "f32_resid"):
-            _close(m32[k], m16[k], tol32, 1e-5, f"mfma32 {k} vs mfma16 (M={M} N={N} K={K})")
-        for k in ("bf16", "bf16_resid", "gelu_a", "gelu_d", "gelu_bwd"):
-            _close(m32[k], m16[k], 1e-3, 8e-3, f"mfma32 {k} vs mfma16 (M={M} N={N} K={K})")
-            frac = (m32[k] != m16[k]).float().mean().item()
-            assert frac < 0.05, f"mfma32 {k}: {frac:.3f} of the bf16 outputs differ from the 16x16x32 form"
-        assert torch.equal(m32["gelu_a"], m32["gelu_nosave"])
-        _close(m32["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "mfma32 EPI_F32 vs fp32")
-        _close(m32["f32_resid"], ref + resid, 1e-4 * math.sqrt(K) * 4, 1e-4, "mfma32 EPI_F32_RESID vs fp32")
-        _close(m32["bf16"], ref, 1e-3, 8e-3, "mfma32 EPI_BF16 vs fp32")
-        _close(m32["gelu_bwd"], (X.float() @ W.float().t()) * dgs.float(), 2e-3, 1.5e-2, "mfma32 EPI_GELU_BWD")
+        outs = {"bf16": ops.linear_fwd(X, W, b, ops.EPI_BF16),
+                "f32": ops.linear_fwd(X, W, b, ops.EPI_F32),
+                "f32_resid": ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid)}
+        gb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.gemm(M, N, K, X, K, True, W, K, True, ops.EPI_GELU_BWD, out=gb, ldc=N, aux=dgs, ldaux=N)
+        d, a = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
+        nosave = ops.linear_fwd(X, W, b, ops.EPI_GELU)[1]
+        torch.cuda.synchronize()
+        assert torch.equal(a, nosave)
+        _close(outs["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "EPI_F32 vs fp32")
+        _close(outs["f32_resid"], ref + resid, 1e-4 * math.sqrt(K) * 4, 1e-4, "EPI_F32_RESID vs fp32")
+        _close(outs["bf16"], ref, 1e-3, 8e-3, "EPI_BF16 vs fp32")
+        _close(gb, (X.float() @ W.float().t()) * dgs.float(), 2e-3, 1.5e-2, "EPI_GELU_BWD")
+        pre = outs["bf16"].float()
+        _close(a, torch.nn.functional.gelu(pre), 2e-3, 1.5e-2, "EPI_GELU vs gelu(bf16 pre-activation)")
 
 
 @pytest.mark.parametrize("K", [32, 64, 96, 384, 1024])

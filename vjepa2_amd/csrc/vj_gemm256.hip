@@ -1,10 +1,7 @@
 // Large-tile bf16 GEMM for gfx950: 256 x BN x 64 tiles (BN = 256 or 128), 512 threads = 8 waves,
-// one workgroup per CU (LDS 144 / 112 KB). Two MFMA forms of the same tile:
-//   M32 = false: v_mfma_f32_16x16x32_bf16, waves 2 (M) x 4 (N), wave tile 128 x 64;
-//   M32 = true : v_mfma_f32_32x32x16_bf16, waves 4 (M) x 2 (N), wave tile 64 x 128 (K-major A and B,
-//                256-wide tiles): each MFMA holds its SIMD's vector-issue port 8 of 32 cycles instead of
-//                8 of 16, so the LDS-DMA issue, fragment reads and barrier of the main loop get 3x
-//                the free issue slots per flop; the same 24 ds_read_b128 per wave and K-tile.
+// one workgroup per CU (LDS 144 / 112 KB), v_mfma_f32_16x16x32_bf16, waves 2 (M) x 4 (N), wave tile
+// 128 x 64. (A 32x32x16 form of the tile, waves 4 x 2, measured no faster per kernel and 3 % slower
+// per train step in round 4 - profiles/r04_gemm_mf32_*.txt - and was removed.)
 // Same operand/epilogue contract as vj_gemm.hip (K-major or MN-major A and B, fused epilogues);
 // used for the forward and data-gradient GEMMs of the encoder / predictor blocks (M = tokens) and the
 // split-K weight gradients.
@@ -29,8 +26,8 @@
 // Schedule choices fixed by round-3 measurements (the variants were removed from the source; the
 // numbers are in DESIGN.md and profiles/r03_gemm_*):
 //  * 8-wave main loop: only the A pieces of K-tile t + 2 go out after the barrier; the B pieces are
-//    issued after 3 of the last phase's 4 m-tiles (SPLIT_AT; 16x16x32 form) or 6 of its 8 MFMAs
-//    (32x32x16 form): -2..-7 % and a further 0..-5 % on the ViT-L shapes (r03_gemm_spread_kernels.txt,
+//    issued after 3 of the last phase's 4 m-tiles (SPLIT_AT): -2..-7 % and a further 0..-5 % on the
+//    ViT-L shapes (r03_gemm_spread_kernels.txt,
 //    r03_gemm_split_kernels.txt). Also the A pieces after the first m-tile: slower.
 //  * on 256-wide bf16 tiles without a VALU-heavy epilogue only waves 0-3 issue the main-loop LDS-DMA
 //    (DMA_WAVES; their SIMD partners keep issuing MFMAs); the next tile's stage 1, issued around the
@@ -40,9 +37,6 @@
 //  * one m-tile of residual / saved-derivative rows prefetched ahead in the direct epilogue (deeper:
 //    no faster, r03 stamps).
 constexpr int SPLIT_AT = 3;
-#ifndef VJ_STG_PRIO  // experiment build: s_setprio 1 around the staggered loop's MFMA intervals
-#define VJ_STG_PRIO 0
-#endif
 constexpr int DMA_WAVES = 4;
 constexpr int AUX_PF = 1;
 
@@ -59,29 +53,25 @@ __device__ long vj_gemm_stamps[2048 * 16 * 4];
 // BMT = 192 (8-wave, K-major bf16, 256-wide direct-store tiles only): 96-row wave tiles (3 m-tiles
 // per M-half) for problems whose 256-row tile count leaves a round of CUs under-filled (context
 // GEMMs, M ~ 11.7k: 184 tiles of 256 x 256 on 256 CUs -> 244 tiles of 192 x 256).
-template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, bool M32 = false,
-          bool STG = false>
+template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, bool STG = false>
 __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
-  static_assert(!STG || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256 && !M32 && EPI != EPI_PARTIAL),
+  static_assert(!STG || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256 && EPI != EPI_PARTIAL),
                 "staggered main loop: 8-wave K-major bf16 256 x 256 tiles");
   static_assert(!F8 || (AK && BKM && EPI != EPI_PARTIAL && EPI != EPI_GELU_BWD), "fp8: forward GEMMs only");
   static_assert(NWV == 8 || (NWV == 4 && AK && BKM && !F8), "2-workgroup GEMM: K-major bf16 operands only");
-  static_assert(!M32 || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256),
-                "32x32x16 form: 8-wave K-major bf16 256 x 256 tiles");
   constexpr int BM = BMT;
   constexpr int MH = BM / 64;     // virtual 16-row m-tiles per half of the wave's rows (4 / 3)
   constexpr int BK = NWV == 8 ? 64 : 32;
   constexpr int NT = NWV * 64;
-  constexpr int WNX = M32 ? 2 : NWV / 2;  // waves across N (16x16x32: 4 / 2, 32x32x16: 2)
+  constexpr int WNX = NWV / 2;  // waves across N (4 / 2)
   constexpr int WMX = NWV / WNX;          // waves across M (2 / 4)
-  constexpr int WM = BM / WMX;            // wave tile rows (128 / 96; 32x32x16: 64)
+  constexpr int WM = BM / WMX;            // wave tile rows (128 / 96)
   constexpr int A_BYTES = BM * BK * 2;
   constexpr int B_BYTES = BN * BK * 2;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int WN = BN / WNX;    // wave tile columns (64 / 32; 32x32x16: 128)
-  constexpr int PB = M32 ? 32 : 16;  // MFMA output block width
+  constexpr int WN = BN / WNX;    // wave tile columns (64 / 32)
+  constexpr int PB = 16;         // MFMA output block width
   constexpr int NTN = WN / PB;    // n blocks per wave (4 / 2)
-  constexpr int MB32 = WM / 32;   // 32x32x16: m blocks per wave (2)
   // LDS-DMA issuers: DMA_WAVES = 4 -> waves 0-3 only on 256-wide tiles (their SIMD partners 4-7 keep
   // issuing MFMAs meanwhile), except the RoPE / GELU / GELU-backward tiles, whose next-tile stage 1
   // goes out right before (or in) their VALU-heavy epilogue, where waves 0-3 would start it 16
@@ -272,21 +262,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     }
   }
 
-  // Accumulators. 16x16x32: acc[i][j] = m-tile i (16 rows), n block j. 32x32x16: acc32[mb][j] = m block
-  // mb (32 rows), n block j. The epilogue walks 2 * MH "virtual m-tiles" of 4 rows per lane either way:
-  // ACC(i, j, r) is lane's value of row r of virtual m-tile i in n block j, ROWOFF(i) that tile's
-  // first row within the wave tile (the lane's 4-row offset comes on top: 4 (lane >> 4) or 4 (lane >> 5)).
-  [[maybe_unused]] f32x4 acc[M32 ? 1 : 2 * MH][NTN];
-  [[maybe_unused]] f32x16 acc32[M32 ? MB32 : 1][NTN];
-  auto accv = [&](int i, int j, int r) -> float {
-    if constexpr (M32) return acc32[i >> 2][j][4 * (i & 3) + r];
-    else return acc[i][j][r];
-  };
-  auto accs = [&](int i, int j, int r, float v) {
-    if constexpr (M32) acc32[i >> 2][j][4 * (i & 3) + r] = v;
-    else acc[i][j][r] = v;
-  };
-  auto rowoff = [](int i) { return M32 ? (i >> 2) * 32 + 8 * (i & 3) : i * 16; };
+  // Accumulators: acc[i][j] = m-tile i (16 rows), n block j; the epilogue walks the 2 * MH m-tiles,
+  // 4 rows per lane (rows rowoff(i) + 4 (lane >> 4) + r of the wave tile).
+  f32x4 acc[2 * MH][NTN];
+  auto accv = [&](int i, int j, int r) -> float { return acc[i][j][r]; };
+  auto accs = [&](int i, int j, int r, float v) { acc[i][j][r] = v; };
+  auto rowoff = [](int i) { return i * 16; };
   bf16x8 Aa[MH], Ab[MH], Ba[NTN], Bb[NTN];
   // A fragments of M-half mh (4 m-tiles), k-step ks; B fragments of all NTN n-tiles, k-step ks
   auto rdA = [&](bf16x8 (&X)[MH], int slot, int mh, int ks) {
@@ -298,27 +279,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     const LDS_AS char* s = smem + slot * STAGE + A_BYTES;
 #pragma unroll
     for (int j = 0; j < NTN; ++j) Y[j] = frag<BKM, BN, BK>(s, wc * WN + j * 16, ks, lane);
-  };
-  // ---- 32x32x16 (M32) fragments of k-step ks (16 deep): lane l reads row (l & 31) of a 32-row block,
-  // 16-B chunk 2 ks + (l >> 5); the K-major swizzle (chunk ^= (row >> 1) & 7) keeps every 16-lane
-  // quarter of a ds_read_b128 on 16 distinct bank slots. A: the wave's MB32 m blocks (into X[0..]),
-  // B: its NTN n blocks (LDS rows wc * 128 + 32 j, permuted at staging: PB = 32).
-  auto rd32 = [&](bf16x8 (&X)[MH], bf16x8 (&Y)[NTN], int slot, int ks) {
-    const LDS_AS char* s = smem + slot * STAGE;
-    const int lr = lane & 31;
-    const int off = lr * 128 + (((2 * ks + (lane >> 5)) ^ ((lr >> 1) & 7)) * 16);
-#pragma unroll
-    for (int i = 0; i < MB32; ++i) X[i] = *(const LDS_AS bf16x8*)(s + (wr * WM + 32 * i) * 128 + off);
-#pragma unroll
-    for (int j = 0; j < NTN; ++j) Y[j] = *(const LDS_AS bf16x8*)(s + A_BYTES + (wc * WN + 32 * j) * 128 + off);
-  };
-  // MFMAs q0 .. q1 - 1 of a k-step (q = mb * NTN + j)
-  auto mm32 = [&](const bf16x8 (&X)[MH], const bf16x8 (&Y)[NTN], int q0, int q1) {
-#pragma unroll
-    for (int q = 0; q < MB32 * NTN; ++q)
-      if (q >= q0 && q < q1)
-        acc32[q / NTN][q % NTN] =
-            __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[q / NTN], Y[q % NTN], acc32[q / NTN][q % NTN], 0, 0, 0);
   };
   // ---- fp8 (F8): one K-tile row is 128 B = 128 e4m3 values = ONE v_mfma_scale_f32_16x16x128_f8f6f4
   // per 16x16 output tile. Its 32-B lane operand is the two 16-B fragments the bf16 path reads for
@@ -400,17 +360,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       const int t = threadIdx.x;
       if (t < BM && cur.m0 + t < g.M) pf_id = g.rope.ids ? g.rope.ids[cur.m0 + t] : (cur.m0 + t) % g.rope.mod;
     }
-    if constexpr (M32) {
 #pragma unroll
-      for (int i = 0; i < MB32; ++i)
+    for (int i = 0; i < 2 * MH; ++i)
 #pragma unroll
-        for (int j = 0; j < NTN; ++j) acc32[i][j] = f32x16{};
-    } else {
-#pragma unroll
-      for (int i = 0; i < 2 * MH; ++i)
-#pragma unroll
-        for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+      for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (F8) {  // this tile's per-row scale exponents (retired by the wait below)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -512,10 +465,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         if (AUX && u == nku - 2) stg_aux();
         if (AUX && nku == 1) stg_aux();
         bar();
-        if (VJ_STG_PRIO) __builtin_amdgcn_s_setprio(1);
         mm(Aa, 0, Ba);
         mm(Ab, 1, Ba);
-        if (VJ_STG_PRIO) __builtin_amdgcn_s_setprio(0);
         if (u + 1 < nku || wr == 0) bar();
       }
     } else {
@@ -524,16 +475,14 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       if constexpr (F8) {
         rdA8(Xa, par, 0);
         rdB8(0, NTN / 2, par);
-      } else if constexpr (M32) {
-        rd32(Aa, Ba, par, 0);
       } else {
         rdA(Aa, par, 0, 0);
         rdB(Ba, par, 0);
       }
 
       // Per K-tile t: 4 phases, each with the fragments of the NEXT phase read while the current
-      // phase's MFMAs run: 16x16x32 (k-step, M-half) = (0,0) (0,1) (1,0) (1,1), 4*NTN MFMAs each;
-      // 32x32x16 k-steps 0..3, 8 MFMAs each. One barrier per tile, before phase 3 (whose prefetch reads
+      // phase's MFMAs run: (k-step, M-half) = (0,0) (0,1) (1,0) (1,1), 4*NTN MFMAs each. One barrier
+      // per tile, before phase 3 (whose prefetch reads
       // tile t+1): it retires this wave's DMA of tile t+1 (issued one tile earlier) and its reads of
       // tile t; then slot (t + par) & 1 is free for the DMA of tile t+2, or of the next tile's stages
       // once this tile has none left.
@@ -541,7 +490,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // 8-wave bf16 main loop: only the A pieces of K-tile t + 2 go out after the barrier; the B pieces
       // are issued inside the last phase's MFMAs (SPLIT: m-tiles / MFMAs before them)
       constexpr bool SPREAD = NWV == 8 && !F8 && BK == 64;
-      constexpr int SPLIT = M32 ? 6 : (MH == 4 ? SPLIT_AT : MH - 1);
+      constexpr int SPLIT = MH == 4 ? SPLIT_AT : MH - 1;
       // one K-tile; TAIL (the last two K-tiles) DMAs the next tile's stages instead of this tile's
       auto ktile = [&](const int t, auto tail_c) {
         constexpr bool TAIL = decltype(tail_c)::value;
@@ -562,20 +511,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           rdA8(Xb, sl, 3);
           __builtin_amdgcn_sched_barrier(0);
           mm8(Xa, 2, 0, NTN);
-          __builtin_amdgcn_sched_barrier(0);
-        } else if constexpr (M32) {
-          // k-steps 0..2 (fragments alternate between (Aa, Ba) and (Ab, Bb))
-          rd32(Ab, Bb, sl, 1);
-          __builtin_amdgcn_sched_barrier(0);
-          mm32(Aa, Ba, 0, 8);
-          __builtin_amdgcn_sched_barrier(0);
-          rd32(Aa, Ba, sl, 2);
-          __builtin_amdgcn_sched_barrier(0);
-          mm32(Ab, Bb, 0, 8);
-          __builtin_amdgcn_sched_barrier(0);
-          rd32(Ab, Bb, sl, 3);
-          __builtin_amdgcn_sched_barrier(0);
-          mm32(Aa, Ba, 0, 8);
           __builtin_amdgcn_sched_barrier(0);
         } else if constexpr (BK == 32) {
           // one k-step: phase 0 = (M-half 0) under the read of M-half 1's A fragments; phase 1 after
@@ -646,20 +581,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           __builtin_amdgcn_sched_barrier(0);
           mm8(Xb, 3, NTN / 2, NTN);
           __builtin_amdgcn_sched_barrier(0);
-        } else if constexpr (M32) {
-          // k-step 3; the next K-tile's k-step 0 fragments are read under it
-          if (t + 1 < nk) rd32(Aa, Ba, sl ^ 1, 0);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (SPREAD && !TAIL) {
-            mm32(Ab, Bb, 0, SPLIT);
-            __builtin_amdgcn_sched_barrier(0);
-            b_pieces();
-            __builtin_amdgcn_sched_barrier(0);
-            mm32(Ab, Bb, SPLIT, 8);
-          } else {
-            mm32(Ab, Bb, 0, 8);
-          }
-          __builtin_amdgcn_sched_barrier(0);
         } else if constexpr (BK == 32) {
           mm(Ab, 1, Ba);
           __builtin_amdgcn_sched_barrier(0);
@@ -701,12 +622,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     asm volatile("" : "+v"(lane_e));
     if constexpr (DIRECT) {
       const int lane = lane_e;
-      const int lrow = M32 ? 4 * (lane >> 5) : 4 * (lane >> 4);  // the lane's row offset in a virtual m-tile
-      // ---- direct epilogue (K-major B staged with PERM): lane (c = lane&15, g = lane>>4; 32x32x16:
-      // c = lane&31, g = lane>>5) owns rows rowoff(i) + 4g + r of virtual m-tile i and the NTN
+      const int lrow = 4 * (lane >> 4);  // the lane's row offset in an m-tile
+      // ---- direct epilogue (K-major B staged with PERM): lane (c = lane&15, g = lane>>4) owns rows
+      // rowoff(i) + 4g + r of m-tile i and the NTN
       // consecutive columns nb .. nb+NTN-1, so every row goes out of registers as one 8/16-B store;
       // no LDS round trip.
-      const int nb = cur.n0 + wc * WN + NTN * (M32 ? (lane & 31) : (lane & 15));
+      const int nb = cur.n0 + wc * WN + NTN * (lane & 15);
       const bool nok = nb < g.N;
       const int mb = cur.m0 + wr * WM + lrow;
       float bias[NTN];
@@ -845,7 +766,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           // turns accv(i, r, 0..3) into row r's 4 columns, bias / residual are added in place (tied
           // adds). Stores read their data registers after issue, so staging copies recycled from row
           // to row cost one memory latency per 16-B store; the accumulators are not reused before the
-          // next tile. (32x32x16: row r's columns are then 4 consecutive registers of acc32[..][r].)
+          // next tile.
 #pragma unroll
           for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -869,10 +790,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
             const int m = mb + rowoff(i) + r;
             if (m < g.M && nok) {
               float* dst = base_f + off_f + (long)(rowoff(i) + r) * ld_f;
-              if constexpr (M32)
-                *(f32x4*)dst = f32x4{accv(i, r, 0), accv(i, r, 1), accv(i, r, 2), accv(i, r, 3)};
-              else
-                *(f32x4*)dst = acc[i][r];
+              *(f32x4*)dst = acc[i][r];
             }
           }
           continue;
@@ -1191,35 +1109,6 @@ bool use_bm192(int M, int tn) {
   return r192 * 192 * 108 < r256 * 256 * 85;
 }
 
-// 32x32x16 form of the 256 x 256 tile (K-major A and B)
-int launch32(int epi, const G256& g, hipStream_t st) {
-  const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
-#define L32(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 256, true>), grid, dim3(512), 0, st, g); break
-  switch (epi) {
-    case EPI_BF16: L32(EPI_BF16);
-    case EPI_F32: L32(EPI_F32);
-    case EPI_F32_RESID: L32(EPI_F32_RESID);
-    case EPI_GELU: L32(EPI_GELU);
-    case EPI_GELU_BWD: L32(EPI_GELU_BWD);
-    case EPI_ROPE: L32(EPI_ROPE);
-    case EPI_BF16_RESID: L32(EPI_BF16_RESID);
-    default: vj_set_error("gemm256(32x32x16): bad epilogue %d", epi); return VJ_ERR_ARG;
-  }
-#undef L32
-  VJ_LAUNCH_CHECK("vj_gemm256(32x32x16)");
-  return VJ_OK;
-}
-
-// MFMA form of a K-major 256 x 256-tile GEMM. VJ_GEMM_MF: 16 = always 16x16x32, 32 = always 32x32x16
-// (where the shape takes 256-row tiles), unset = the measured default (GEMM).
-bool use_m32(int epi) {
-  const char* e = getenv("VJ_GEMM_MF");
-  if (e && e[0] == '3') return true;
-  if (e && e[0] == '1') return false;
-  (void)epi;
-  return false;
-}
-
 // Staggered main loop (STG) for the K-major 256 x 256-tile GEMMs with K % 32 == 0. VJ_GEMM_STG: 0 = never,
 // 1 = always (where the shape takes 256-row tiles), unset = the measured default: the epilogues that
 // read no aux rows (GELU, RoPE, bf16 / f32 out). Measured in the train step (rocprofv3, one call,
@@ -1235,7 +1124,7 @@ bool use_stg(int K, int epi) {
 
 int launch_stg(int epi, const G256& g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
-#define LSTG(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 256, false, true>), grid, dim3(512), 0, st, g); break
+#define LSTG(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 256, true>), grid, dim3(512), 0, st, g); break
   switch (epi) {
     case EPI_BF16: LSTG(EPI_BF16);
     case EPI_F32: LSTG(EPI_F32);
@@ -1315,7 +1204,6 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
       g.group = tile_group(g.tiles_m, tn);
       return launch192(epi, g, st);
     }
-    if (a_kmajor && b_kmajor && use_m32(epi)) return launch32(epi, g, st);
     if (a_kmajor && b_kmajor && use_stg(K, epi)) return launch_stg(epi, g, st);
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
     if (a_kmajor && !b_kmajor) return launch256<true, false, 256>(epi, g, st);

@@ -24,8 +24,9 @@ def name_regex(label):
     m = re.fullmatch(r"k_gemm<(\d),(\d),(\w+)>", label)
     if m:
         b = {"1": "true", "0": "false"}
-        # every tile width, the 8-wave and the two-workgroups-per-CU (", false, 4") instantiations
-        return re.compile(rf"k_gemm256<{b[m[1]]}, {b[m[2]]}, {EPI[m[3]]}, \d+(, false)?(, \d+)*>")
+        # every tile width, the 8-wave, two-workgroups-per-CU (", false, 4"), 192-row and staggered
+        # (trailing ", true") instantiations
+        return re.compile(rf"k_gemm256<{b[m[1]]}, {b[m[2]]}, {EPI[m[3]]}, \d+(, (?:true|false|\d+))*>")
     return re.compile(re.escape(label.split("<")[0]) + r"\b")
 
 

@@ -213,10 +213,10 @@ def main():
             roof["traffic_unit"] = "B/launch"
             roof["traffic_source"] = tr["source"]
 
-    # With VJ_TGT_STREAM=1 the target encoder's forward runs on a side stream (train.py), so inside
-    # the timed region the dominant kernel shares the CUs with it. One more UNTIMED step with the side
-    # stream off then gives the same kernel's unshared launch duration.
-    if roof and os.environ.get("VJ_TGT_STREAM", "0") == "1":
+    # By default (VJ_TGT_STREAM unset or 1) the target encoder's forward runs on a side stream
+    # (train.py), so inside the timed region the dominant kernel shares the CUs with it. One more
+    # UNTIMED step with the side stream off then gives the same kernel's unshared launch duration.
+    if roof and os.environ.get("VJ_TGT_STREAM", "1") == "1":
         solo = ops.KernelEvents(only={dom})
         os.environ["VJ_TGT_STREAM"] = "0"
         torch.cuda.synchronize()

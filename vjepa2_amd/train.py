@@ -187,10 +187,11 @@ class JEPATrainer:
         return loss, zp, dz
 
     def _side_stream(self):
-        # Off by default: measured on MI355X it recovered ~1 % of the step while inflating the
-        # memory-bound kernels it shares CUs with (profiles/r01_kernel_stats*.txt). VJ_TGT_STREAM=1
-        # turns it on.
-        if os.environ.get("VJ_TGT_STREAM", "0") != "1" or not torch.cuda.is_available():
+        # On by default since round 4: with the persistent one-workgroup-per-CU GEMMs and the faster
+        # epilogues the overlap is worth +2.0 % clips/s (207.5 / 207.6 -> 211.5 / 211.7, bench.py A/B
+        # in one call, profiles/r04_tgt_stream_step_ab.txt); in round 1 it gave ~1 % while inflating
+        # the memory-bound kernels it shared CUs with. VJ_TGT_STREAM=0 runs everything on one stream.
+        if os.environ.get("VJ_TGT_STREAM", "1") != "1" or not torch.cuda.is_available():
             return None
         if getattr(self, "_tgt_stream", None) is None:
             self._tgt_stream = torch.cuda.Stream()

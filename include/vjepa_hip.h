@@ -41,9 +41,9 @@ enum {
 };
 
 /* C[m,n] = sum_k A(m,k) B(n,k) (+ epilogue), bf16 operands, f32 accumulate. M >= 1024 runs the 256-row
- * tile kernels on v_mfma_f32_16x16x32_bf16 (vj_gemm256.hip; vj_gemm_pp.hip, the two-wave-group
- * ping-pong, when VJ_GEMM_PP / VJ_GEMM_PP_EPIS select it), smaller
- * M the 128-row kernel on v_mfma_f32_32x32x16_bf16 (vj_gemm.hip).
+ * tile kernels on v_mfma_f32_16x16x32_bf16 (vj_gemm256.hip: the one-tile main loop, or the staggered
+ * one for the K-major 256-wide GELU / RoPE / bf16 / f32 GEMMs), smaller M the 128-row kernel on
+ * v_mfma_f32_32x32x16_bf16 (vj_gemm.hip).
  * A(m,k) = a_kmajor ? A[m*lda+k] : A[k*lda+m];  B(n,k) = b_kmajor ? B[n*ldb+k] : B[k*ldb+n].
  * Replaces nn.Linear forward/backward (modules.py:77-83, 330, 379-381; predictor.py:182, 244) and the
  * Conv3d tubelet projection as a GEMM over im2col rows (patch_embed.py:42-52). */

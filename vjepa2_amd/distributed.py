@@ -96,7 +96,18 @@ class GradReducer:
         self.next = 0
 
     def _issue(self, b):
-        b.work = dist.all_reduce(b.view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        # With the weight-gradient stream on (functions.wgrad_stream), the bucket's weight gradients
+        # may still be in flight there: issue from that stream after it has waited for the current
+        # one (the LayerNorm / bias gradients written there), so the collective sees both.
+        from .functions import wgrad_stream
+
+        side = wgrad_stream()
+        if side is None:
+            b.work = dist.all_reduce(b.view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            return
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            b.work = dist.all_reduce(b.view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def mark_ready(self, module):
         """Hook called when `module`'s backward has finished writing its parameter gradients."""

@@ -10,6 +10,7 @@ operand is bf16 with f32 accumulation. Parameter gradients are accumulated (+=) 
 autograd only carries activation gradients between layers.
 """
 
+import os
 import weakref
 
 import torch
@@ -264,6 +265,74 @@ def patch_embed_forward_f32(clip, pe, masks, pos_table=None, pos_ids=None, pos_m
     return x
 
 
+# ------------------------------------------------------------------------------------------------
+# Weight-gradient stream. In a block's backward the weight-gradient GEMMs (with their split-K
+# reduction) and the fc1 / qkv bias column sums feed nothing but the gradient arena, while the data
+# gradients form the critical path (dgrad -> LayerNorm backward -> dgrad -> attention backward -> ...).
+# With VJ_WGRAD_STREAM=1 they are issued on a second HIP stream (after everything the current stream
+# has issued so far, their operands' memory held for it with record_stream), so they fill the CUs the
+# critical path leaves idle. Whoever reads the gradients after the backward waits for that stream:
+# the first use queues an autograd end-of-backward callback that makes the current stream wait, and
+# the gradient all-reduce issues its buckets from the wgrad stream (distributed.GradReducer).
+
+_WG_STREAMS = {}
+
+
+def wgrad_stream():
+    """The per-device weight-gradient stream, or None when disabled (VJ_WGRAD_STREAM != 1)."""
+    if os.environ.get("VJ_WGRAD_STREAM", "0") != "1" or not torch.cuda.is_available():
+        return None
+    dev = torch.cuda.current_device()
+    s = _WG_STREAMS.get(dev)
+    if s is None:
+        s = _WG_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
+def join_wgrad_stream():
+    """Make the current stream wait for every weight-gradient launch issued so far."""
+    s = _WG_STREAMS.get(torch.cuda.current_device()) if torch.cuda.is_available() else None
+    if s is not None:
+        torch.cuda.current_stream().wait_stream(s)
+
+
+_WG_JOIN_QUEUED = [False]
+
+
+def _join_at_backward_end():
+    _WG_JOIN_QUEUED[0] = False
+    join_wgrad_stream()
+
+
+class _OnWgradStream:
+    """`with _OnWgradStream(*tensors):` the enclosed launches go to the weight-gradient stream (when
+    enabled), ordered after everything issued so far on the current stream."""
+
+    def __init__(self, *tensors):
+        self.tensors = tensors
+        self.side = wgrad_stream()
+        self.ctx = None
+
+    def __enter__(self):
+        if self.side is None:
+            return self
+        self.side.wait_stream(torch.cuda.current_stream())
+        for t in self.tensors:
+            t.record_stream(self.side)
+        if not _WG_JOIN_QUEUED[0] and torch.is_grad_enabled() is False:
+            # inside an autograd backward (grad mode is off there): join when the whole pass ends
+            torch.autograd.Variable._execution_engine.queue_callback(_join_at_backward_end)
+            _WG_JOIN_QUEUED[0] = True
+        self.ctx = torch.cuda.stream(self.side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
+
+
 def _bias_buf(lin):
     return grad_buf(lin.bias) if lin.bias is not None and lin.bias.requires_grad else None
 
@@ -287,26 +356,31 @@ def block_backward(dxo, blk, lay, saved):
     hd = D // H
     twin = getattr(dxo, "_vj_grad_bf16", None)  # bf16 twin written by the next block's LN1 backward,
     dxo_b = twin[0] if twin is not None and twin[1] == dxo._version else ops.cast_bf16(dxo)  # unless changed since
-    # MLP
+    # MLP (each weight gradient is issued before the data gradient that shares its dY, so on the
+    # weight-gradient stream the two overlap)
+    with _OnWgradStream(dxo_b, act):
+        wgrad(dxo_b, act, mlp.fc2.weight)  # fc2 bias grad: fused into LN2 backward
     dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
-    wgrad(dxo_b, act, mlp.fc2.weight)  # fc2 bias grad: fused into LN2 backward
+    with _OnWgradStream(dpre, ln2):
+        wgrad(dpre, ln2, mlp.fc1.weight)
+        _bias_grad(mlp.fc1, dpre)
     dln2 = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
-    wgrad(dpre, ln2, mlp.fc1.weight)
-    _bias_grad(mlp.fc1, dpre)
     gw, gb = _ln_grads(blk.norm2)
     dxm, dxm_b = ops.layernorm_bwd(dln2, x_mid, m2, r2, blk.norm2.weight, dres_in=dxo, dweight=gw, dbias=gb,
                                    want_bf16=True, sum_in=_bias_buf(mlp.fc2), sum_out=_bias_buf(attn.proj))
     # attention (proj bias grad = column sums of dxm, produced above)
+    with _OnWgradStream(dxm_b, o):
+        wgrad(dxm_b, o, attn.proj.weight)
     do = ops.linear_dgrad(dxm_b, weight_bf16(attn.proj.weight), wt=weight_bf16_t(attn.proj.weight))
-    wgrad(dxm_b, o, attn.proj.weight)
     rope = None
     if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
     dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk)
+    with _OnWgradStream(dqkv, ln1):
+        wgrad(dqkv, ln1, attn.qkv.weight)
+        _bias_grad(attn.qkv, dqkv)
     dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
-    wgrad(dqkv, ln1, attn.qkv.weight)
-    _bias_grad(attn.qkv, dqkv)
     gw, gb = _ln_grads(blk.norm1)
     dxi, dxi_b = ops.layernorm_bwd(dln1, x, m1, r1, blk.norm1.weight, dres_in=dxm, dweight=gw, dbias=gb,
                                    want_bf16=True)

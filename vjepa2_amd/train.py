@@ -29,7 +29,7 @@ from . import predictor as vit_pred
 from . import vision_transformer as video_vit
 from .arena import FlatArena, FusedAdamW, fused_ema, readiness_order, wd_split
 from .distributed import GradReducer, init_distributed
-from .functions import refresh_weight_transposes
+from .functions import join_wgrad_stream, refresh_weight_transposes
 from .masks import MaskCollator, materialize
 from .schedulers import CosineWDSchedule, WarmupCosineSchedule
 from .wrappers import MultiSeqWrapper, PredictorMultiSeqWrapper
@@ -223,6 +223,7 @@ class JEPATrainer:
             zp.backward(dz)
             total = loss if total is None else total + loss
         self._groups = G
+        join_wgrad_stream()  # weight gradients issued on the side stream (no-op when off)
         for a in self.opt.arenas:  # lazily zeroed gradients nothing wrote (before the tail buckets)
             a.finalize_grads()
         ev = None

@@ -274,13 +274,15 @@ def patch_embed_forward_f32(clip, pe, masks, pos_table=None, pos_ids=None, pos_m
 # critical path leaves idle. Whoever reads the gradients after the backward waits for that stream:
 # the first use queues an autograd end-of-backward callback that makes the current stream wait, and
 # the gradient all-reduce issues its buckets from the wgrad stream (distributed.GradReducer).
+# On by default: +2.0 % clips/s (207.2 / 206.8 -> 211.5 / 210.6, bench.py A/B in one call,
+# profiles/r04_wgrad_stream_step_ab.txt); VJ_WGRAD_STREAM=0 keeps everything on one stream.
 
 _WG_STREAMS = {}
 
 
 def wgrad_stream():
-    """The per-device weight-gradient stream, or None when disabled (VJ_WGRAD_STREAM != 1)."""
-    if os.environ.get("VJ_WGRAD_STREAM", "0") != "1" or not torch.cuda.is_available():
+    """The per-device weight-gradient stream, or None when disabled (VJ_WGRAD_STREAM=0)."""
+    if os.environ.get("VJ_WGRAD_STREAM", "1") != "1" or not torch.cuda.is_available():
         return None
     dev = torch.cuda.current_device()
     s = _WG_STREAMS.get(dev)
@@ -296,11 +298,11 @@ def join_wgrad_stream():
         torch.cuda.current_stream().wait_stream(s)
 
 
-_WG_JOIN_QUEUED = [False]
+_WG_JOIN_TASK = [None]  # autograd graph task whose end-of-backward join is queued
 
 
 def _join_at_backward_end():
-    _WG_JOIN_QUEUED[0] = False
+    _WG_JOIN_TASK[0] = None
     join_wgrad_stream()
 
 
@@ -319,10 +321,12 @@ class _OnWgradStream:
         self.side.wait_stream(torch.cuda.current_stream())
         for t in self.tensors:
             t.record_stream(self.side)
-        if not _WG_JOIN_QUEUED[0] and torch.is_grad_enabled() is False:
-            # inside an autograd backward (grad mode is off there): join when the whole pass ends
+        task = torch._C._current_graph_task_id()
+        self.join_on_exit = task == -1  # called outside an autograd backward: join right away
+        if task != -1 and _WG_JOIN_TASK[0] != task:
+            # inside an autograd backward: join once, when the whole pass ends
             torch.autograd.Variable._execution_engine.queue_callback(_join_at_backward_end)
-            _WG_JOIN_QUEUED[0] = True
+            _WG_JOIN_TASK[0] = task
         self.ctx = torch.cuda.stream(self.side)
         self.ctx.__enter__()
         return self
@@ -330,6 +334,8 @@ class _OnWgradStream:
     def __exit__(self, *exc):
         if self.ctx is not None:
             self.ctx.__exit__(*exc)
+            if self.join_on_exit:
+                join_wgrad_stream()
         return False
 
 

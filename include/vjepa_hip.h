@@ -193,6 +193,22 @@ int vj_transpose_bf16(int rows, int cols, const void* src, long ld_src, void* ds
  * each matrix meets vj_transpose_bf16's constraints. Replaces one vj_transpose_bf16 launch per weight. */
 int vj_transpose_bf16_batch(int n, const long* desc, long total_tiles, void* stream);
 
+/* Block variants off the shipped configs (vj_variants.hip), bf16-autocast rounding points.
+ * SwiGLU gate (SwiGLUFFN.forward, src/models/utils/modules.py:102-106): x12 = [M][2h] bf16 holding
+ * fc1(x) | fc2(x); out[m][c] = bf16(bf16(silu(x1)) * x2). Backward: dh [M][h] -> dx12 = dx1 | dx2
+ * (mul backward, then silu_backward). h, strides multiples of 8, pointers 16-B aligned. */
+int vj_swiglu_fwd(int M, int h, const void* x12, long ld, void* out, long ldo, void* stream);
+int vj_swiglu_bwd(int M, int h, const void* dh, long lddh, const void* x12, long ld, void* dx12, long lddx,
+                  void* stream);
+/* Stochastic depth (timm drop_path, applied in Block.forward modules.py:561-562): per-row factor
+ * scale[m] (0 or 1 / keep, the sample's draw repeated over its tokens).
+ * vj_rowscale_add: out = resid + bf16(bf16(y) * bf16(scale[m])), y f32 [M][N] (the branch's output
+ * projection), resid / out f32 or, bf16_resid = 1, bf16. vj_rowscale_bf16: out bf16 = bf16(bf16(dx) *
+ * bf16(scale[m])) (the branch's dY in the backward). N, strides multiples of 4. */
+int vj_rowscale_add(int M, int N, const float* y, long ldy, const float* scale, const void* resid, long ldr, void* out,
+                    long ldo, int bf16_resid, void* stream);
+int vj_rowscale_bf16(int M, int N, const float* dx, long ld, const float* scale, void* out, long ldo, void* stream);
+
 /* JEPA multi-block 3-D masks on the device (src/masks/multiseq_multiblock3d.py:155-239): the host
  * makes the reference's RNG draws (block size, (start, top, left) per block: boxes int32
  * [B][npred][3]); vj_mask_count writes each sample's kept-token count, vj_mask_emit the ascending

@@ -95,14 +95,26 @@ def attention(x, sd, prefix, num_heads, ids=None, tokens_per_frame=None, tokens_
     return F.linear(o, sd[prefix + "proj.weight"], sd[prefix + "proj.bias"])
 
 
-# src/models/utils/modules.py:556-563 (Block) with MLP :77-83 (GELU exact)
-def block(x, sd, prefix, num_heads, eps=1e-6, **rope_kw):
+# src/models/utils/modules.py:77-83 (MLP, GELU exact) / :102-106 (SwiGLUFFN: state dict with fc3)
+def mlp(y, sd, prefix):
+    if prefix + "fc3.weight" in sd:
+        h = F.silu(F.linear(y, sd[prefix + "fc1.weight"], sd[prefix + "fc1.bias"]))
+        h = h * F.linear(y, sd[prefix + "fc2.weight"], sd[prefix + "fc2.bias"])
+        return F.linear(h, sd[prefix + "fc3.weight"], sd[prefix + "fc3.bias"])
+    y = F.gelu(F.linear(y, sd[prefix + "fc1.weight"], sd[prefix + "fc1.bias"]))
+    return F.linear(y, sd[prefix + "fc2.weight"], sd[prefix + "fc2.bias"])
+
+
+# src/models/utils/modules.py:556-563 (Block). draws = the drop_path per-sample scales (timm
+# drop_path: Bernoulli(1 - p) / (1 - p)) of the attention and MLP branches, [B] each, or None.
+def block(x, sd, prefix, num_heads, eps=1e-6, draws=None, **rope_kw):
     D = x.shape[-1]
     y = F.layer_norm(x, (D,), sd[prefix + "norm1.weight"], sd[prefix + "norm1.bias"], eps)
-    x = x + attention(y, sd, prefix + "attn.", num_heads, **rope_kw)
+    y = attention(y, sd, prefix + "attn.", num_heads, **rope_kw)
+    x = x + (y if draws is None else y * draws[0].view(-1, 1, 1))
     y = F.layer_norm(x, (D,), sd[prefix + "norm2.weight"], sd[prefix + "norm2.bias"], eps)
-    y = F.gelu(F.linear(y, sd[prefix + "mlp.fc1.weight"], sd[prefix + "mlp.fc1.bias"]))
-    return x + F.linear(y, sd[prefix + "mlp.fc2.weight"], sd[prefix + "mlp.fc2.bias"])
+    y = mlp(y, sd, prefix + "mlp.")
+    return x + (y if draws is None else y * draws[1].view(-1, 1, 1))
 
 
 # ------------------------------------------------------------------------------------------------

@@ -5,7 +5,8 @@ This script is the only place the reference (weipeilun/vjepa2, mounted read-only
 writes are plain tensors (torch.save of dicts of tensors / python scalars, loaded back with
 ``torch.load(..., weights_only=True)``). No reference source is copied: only inputs and outputs.
 
-Stubs: ``timm.models.layers.drop_path`` (never called at drop_path_rate=0) and
+Stubs: ``timm.models.layers.drop_path`` (timm's published algorithm restated; inert at
+drop_path_rate=0, which every fixture but gen_block_variants' uses) and
 ``app.vjepa.transforms.make_transforms`` (torchvision absent; synthetic clips need no augmentation).
 
 Usage:  python tests/golden/make_golden.py            (writes tests/golden/*.pt)
@@ -29,8 +30,21 @@ timm_models = types.ModuleType("timm.models")
 timm_layers = types.ModuleType("timm.models.layers")
 
 
-def _drop_path(x, drop_prob=0.0, training=False):  # inert at rate 0
-    return x
+_DP = {"gen": None, "log": []}  # drop_path draws: seeded generator, and every draw made (fixture data)
+
+
+def _drop_path(x, drop_prob=0.0, training=False, scale_by_keep=True):
+    """timm.layers.drop_path (timm 0.9.x; absent here), restated: per-sample Bernoulli(keep) mask,
+    scaled by 1 / keep. Inert at rate 0 / eval (every fixture but the drop_path blocks)."""
+    if drop_prob == 0.0 or not training:
+        return x
+    keep_prob = 1 - drop_prob
+    shape = (x.shape[0],) + (1,) * (x.ndim - 1)
+    random_tensor = x.new_empty(shape).bernoulli_(keep_prob, generator=_DP["gen"])
+    if keep_prob > 0.0 and scale_by_keep:
+        random_tensor.div_(keep_prob)
+    _DP["log"].append(random_tensor.flatten().clone())
+    return x * random_tensor
 
 
 timm_layers.drop_path = _drop_path
@@ -106,6 +120,33 @@ def gen_block(name, dim, heads, grid, T, N, K, with_thw, seed):
     save(name, dict(state={k: v.detach().clone() for k, v in blk.state_dict().items()}, x=x.detach(),
                     mask=mask, y=y.detach(), gy=gy, gx=x.grad.detach(), gparams=grads_of(blk),
                     cfg=dict(dim=dim, heads=heads, grid=grid, T=T, with_thw=with_thw)))
+
+
+def gen_block_variants():
+    """Block variants the shipped configs leave off: SwiGLU MLP (act_layer=nn.SiLU -> SwiGLUFFN,
+    modules.py:86-106, wide / narrow hidden) and stochastic depth (drop_path > 0, modules.py:546-562),
+    in training mode; the per-sample drop_path draws (attn branch, then MLP branch) are saved."""
+    for name, act, wide, dp, B, seed in (("block_swiglu.pt", torch.nn.SiLU, True, 0.0, 2, 11),
+                                         ("block_droppath.pt", torch.nn.GELU, True, 0.5, 4, 12),
+                                         ("block_swiglu_dp.pt", torch.nn.SiLU, False, 0.4, 4, 14)):
+        torch.manual_seed(seed)
+        blk = Block(dim=64, num_heads=2, mlp_ratio=4.0, qkv_bias=True, use_rope=True, grid_size=4, act_layer=act,
+                    wide_silu=wide, drop_path=dp, norm_layer=lambda d: torch.nn.LayerNorm(d, eps=1e-6), use_sdpa=True)
+        for p in blk.parameters():
+            with torch.no_grad():
+                p.add_(0.05 * torch.randn_like(p))
+        g = torch.Generator().manual_seed(seed + 1)
+        x = torch.randn(B, 10, 64, generator=g, requires_grad=True)
+        mask = sorted_unique_rows(B, 10, 32, g)
+        _DP["gen"], _DP["log"] = torch.Generator().manual_seed(seed + 2), []
+        y = blk(x, mask=mask, T=2, H_patches=4, W_patches=4)
+        draws = list(_DP["log"])
+        gy = torch.randn(y.shape, generator=g)
+        y.backward(gy)
+        save(name, dict(state={k: v.detach().clone() for k, v in blk.state_dict().items()}, x=x.detach(),
+                        mask=mask, y=y.detach(), gy=gy, gx=x.grad.detach(), gparams=grads_of(blk),
+                        draws=draws, cfg=dict(dim=64, heads=2, grid=4, T=2, silu=act is torch.nn.SiLU,
+                                              wide_silu=wide, drop_path=dp, seed=seed)))
 
 
 def gen_encoder():
@@ -539,6 +580,7 @@ if __name__ == "__main__":
     gen_sincos()
     gen_block("block_enc.pt", dim=128, heads=2, grid=4, T=2, N=32, K=10, with_thw=True, seed=3)
     gen_block("block_pred.pt", dim=96, heads=3, grid=4, T=2, N=32, K=9, with_thw=False, seed=4)
+    gen_block_variants()
     gen_encoder()
     gen_predictor()
     gen_masks()

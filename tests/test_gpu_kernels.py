@@ -831,3 +831,59 @@ def test_refresh_weight_transposes_matches_lazy_copies():
     assert w._vj_bf16_t[0][1] == F.SHADOW_EPOCH[0]
     assert torch.equal(w._vj_bf16_t[1], w._vj_bf16.t().contiguous())
     assert F.weight_bf16_t(w) is w._vj_bf16_t[1]
+
+
+# ------------------------------------------------------------------------------------------------
+# Block variants (vj_variants.hip): SwiGLU gate, drop_path row scaling. Expected values are the
+# reference's own bf16 autocast ops (torch elementwise kernels on the same bf16 inputs).
+@pytest.mark.parametrize("M,h", [(1, 8), (37, 344), (1000, 1368)])
+def test_swiglu_gate_vs_torch_bf16(M, h):
+    from vjepa2_amd import ops
+
+    torch.manual_seed(M + h)
+    x12 = (2.5 * torch.randn(M, 2 * h, device=DEV)).bfloat16()
+    x1 = x12[:, :h].clone().requires_grad_(True)
+    x2 = x12[:, h:].clone().requires_grad_(True)
+    ref = torch.nn.functional.silu(x1) * x2  # SwiGLUFFN.forward, modules.py:103-105, bf16 tensors
+    got = ops.swiglu_fwd(x12)
+    # silu in f32 then bf16: the device expf may differ from torch's by an f32 ulp -> at most 1 bf16 ulp
+    _close(got, ref, 0.0, 2.0**-7, "swiglu fwd")
+    assert (got.float() == ref.detach().float()).float().mean().item() > 0.99
+    dh = torch.randn(M, h, device=DEV).bfloat16()
+    ref.backward(dh)
+    dx12 = ops.swiglu_bwd(dh, x12)
+    _close(dx12[:, :h], x1.grad, 1e-30, 2.0**-6, "swiglu dx1")
+    _close(dx12[:, h:], x2.grad, 1e-30, 2.0**-7, "swiglu dx2")
+
+
+@pytest.mark.parametrize("bf16_resid", [False, True])
+def test_rowscale_kernels_exact(bf16_resid):
+    """vj_rowscale_add / vj_rowscale_bf16 against the same bf16-rounded arithmetic in torch: bit-exact."""
+    from vjepa2_amd import ops
+
+    torch.manual_seed(3)
+    M, N = 777, 136
+    y = torch.randn(M, N, device=DEV)
+    keep = 0.6
+    s = (torch.rand(M, device=DEV) < keep).bfloat16().div_(keep).float()
+    resid = torch.randn(M, N, device=DEV)
+    resid = resid.bfloat16() if bf16_resid else resid
+    got = ops.rowscale_add(y, s, resid)
+    branch = (y.bfloat16() * s.bfloat16()[:, None]).float()  # bf16 * bf16 -> bf16 (f32 math, one rounding)
+    exp = resid.float() + branch
+    exp = exp.bfloat16() if bf16_resid else exp
+    assert got.dtype == resid.dtype and torch.equal(got, exp)
+    dx = torch.randn(M, N, device=DEV)
+    assert torch.equal(ops.rowscale_bf16(dx, s), dx.bfloat16() * s.bfloat16()[:, None])
+
+
+def test_drop_path_sample_distribution():
+    """DropPath.sample: the reference's random_tensor values (0 or bf16(1 / keep)) at rate ~keep."""
+    from vjepa2_amd.modules import DropPath
+
+    torch.manual_seed(0)
+    dp = DropPath(0.3)
+    r = dp.sample(200000, DEV)
+    vals = set(r.unique().tolist())
+    assert vals == {0.0, torch.tensor(1 / 0.7).bfloat16().item()} or vals == {0.0, (torch.tensor(1.0).bfloat16() / 0.7).item()}
+    assert abs((r > 0).float().mean().item() - 0.7) < 0.005

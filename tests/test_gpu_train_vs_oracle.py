@@ -12,8 +12,9 @@ from oracle import vjepa_oracle as orc
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("bf16_target", [True, False])
-def test_train_step_vs_oracle(bf16_target):
+@pytest.mark.parametrize("bf16_target,silu", [(True, False), (False, False), (True, True)])
+def test_train_step_vs_oracle(bf16_target, silu):
+    """silu: encoder and predictor on the SwiGLU MLP (model.use_silu / use_pred_silu, wide_silu)."""
     from vjepa2_amd.masks import MaskCollator
     from vjepa2_amd.train import JEPATrainer, init_opt, init_video_model
 
@@ -22,7 +23,9 @@ def test_train_step_vs_oracle(bf16_target):
     T, S, B = 8, 64, 2
     enc, pred = init_video_model(device=dev, patch_size=16, max_num_frames=T, tubelet_size=2, model_name="vit_small",
                                  crop_size=S, pred_depth=2, pred_num_heads=12, pred_embed_dim=384, uniform_power=True,
-                                 use_mask_tokens=True, num_mask_tokens=2, use_sdpa=True, use_rope=True)
+                                 use_mask_tokens=True, num_mask_tokens=2, use_sdpa=True, use_rope=True,
+                                 use_silu=silu, use_pred_silu=silu, wide_silu=True)
+    assert silu == hasattr(enc.backbone.blocks[0].mlp, "fc3") == hasattr(pred.backbone.predictor_blocks[0].mlp, "fc3")
     enc_sd = {k: v.detach().cpu().clone() for k, v in enc.backbone.state_dict().items()}
     pred_sd = {k: v.detach().cpu().clone() for k, v in pred.backbone.state_dict().items()}
     tgt = copy.deepcopy(enc)
@@ -47,7 +50,7 @@ def test_train_step_vs_oracle(bf16_target):
     w = enc.backbone.blocks[0].attn.qkv.weight.detach().cpu()
     w0 = enc_sd["blocks.0.attn.qkv.weight"]
     agree = (torch.sign(w - w0) == torch.sign(ref.enc["blocks.0.attn.qkv.weight"].detach() - w0)).float().mean().item()
-    print(f"bf16 target residual={bf16_target}: loss {loss:.6f} vs oracle {ref_loss:.6f} (rel {rel:.2e}), "
+    print(f"bf16 target residual={bf16_target} silu={silu}: loss {loss:.6f} vs oracle {ref_loss:.6f} (rel {rel:.2e}), "
           f"AdamW update sign agreement {agree:.4f}")
     assert rel < 1e-2
     assert agree > 0.9

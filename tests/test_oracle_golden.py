@@ -43,15 +43,19 @@ def test_product_sincos_table_matches_reference():
         assert torch.equal(torch.from_numpy(sincos_3d_table(96, 4, 2, bool(up))), g[f"f64_up{up}"])
 
 
-@pytest.mark.parametrize("fixture", ["block_enc.pt", "block_pred.pt"])
+@pytest.mark.parametrize("fixture", ["block_enc.pt", "block_pred.pt", "block_swiglu.pt", "block_droppath.pt",
+                                     "block_swiglu_dp.pt"])
 def test_block_golden(fixture):
+    """Block (modules.py:500-563), incl. the SwiGLU MLP and drop_path variants (their per-sample
+    draws replayed from the fixture)."""
     g = gold(fixture)
     c = g["cfg"]
     sd = {k: v.clone().requires_grad_(True) for k, v in g["state"].items()}
     x = g["x"].clone().requires_grad_(True)
     grid = c["grid"]
     tpf, tpr = grid * grid, grid  # with T/H/W given the same square grid results
-    y = orc.block(x, sd, "", c["heads"], ids=g["mask"], tokens_per_frame=tpf, tokens_per_row=tpr)
+    draws = g["draws"] if g.get("draws") else None
+    y = orc.block(x, sd, "", c["heads"], ids=g["mask"], tokens_per_frame=tpf, tokens_per_row=tpr, draws=draws)
     close(y, g["y"], 1e-5, "block y")
     y.backward(g["gy"])
     close(x.grad, g["gx"], 1e-5, "block dx")
@@ -212,3 +216,27 @@ def test_vitl_seeded_init_matches_reference():
     assert set(sd) == set(d["param_sums"])
     for k, v in sd.items():
         assert abs(float(v.double().sum()) - d["param_sums"][k]) <= 1e-9 * (1 + abs(d["param_sums"][k])), k
+
+
+@pytest.mark.parametrize("fixture", ["block_swiglu.pt", "block_droppath.pt", "block_swiglu_dp.pt"])
+def test_variant_block_seeded_init_matches_reference(fixture):
+    """vjepa2_amd.modules.Block with SwiGLU / drop_path builds the reference's parameters with the same
+    RNG consumption: under the fixture's seed (and the generator's perturbation) every tensor of the
+    state dict is bitwise the reference's."""
+    import torch.nn as nn
+
+    from vjepa2_amd.modules import Block
+
+    g = gold(fixture)
+    c = g["cfg"]
+    torch.manual_seed(c["seed"])
+    blk = Block(dim=c["dim"], num_heads=c["heads"], mlp_ratio=4.0, qkv_bias=True, use_rope=True, grid_size=c["grid"],
+                act_layer=nn.SiLU if c["silu"] else nn.GELU, wide_silu=c["wide_silu"], drop_path=c["drop_path"],
+                norm_layer=lambda d: nn.LayerNorm(d, eps=1e-6))
+    for p in blk.parameters():
+        with torch.no_grad():
+            p.add_(0.05 * torch.randn_like(p))
+    sd = blk.state_dict()
+    assert list(sd) == list(g["state"])
+    for k, v in g["state"].items():
+        assert torch.equal(sd[k], v), k

@@ -62,6 +62,10 @@ SIGNATURES = {
     "vj_cast_bf16": [_L, _P, _P, _P],
     "vj_transpose_bf16": [_I, _I, _P, _L, _P, _L, _P],
     "vj_transpose_bf16_batch": [_I, _P, _L, _P],
+    "vj_swiglu_fwd": [_I, _I, _P, _L, _P, _L, _P],
+    "vj_swiglu_bwd": [_I, _I, _P, _L, _P, _L, _P, _L, _P],
+    "vj_rowscale_add": [_I, _I, _P, _L, _P, _P, _L, _P, _L, _I, _P],
+    "vj_rowscale_bf16": [_I, _I, _P, _L, _P, _P, _L, _P],
     "vj_xattn_ws_floats": [_I, _I, _I, _I, _I, ctypes.POINTER(_L)],
     "vj_xattn_fwd": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _P, _F, _P, _L, _P],
     "vj_xattn_bwd": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _P, _L, _P, _F, _P, _L, _P, _L, _P, _L, _P],

@@ -14,7 +14,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvjepa_hip.so")
-SOURCES = ["vj_capi.hip", "vj_gemm.hip", "vj_gemm256.hip", "vj_attn.hip", "vj_ops.hip", "vj_f32.hip", "vj_xattn.hip"]
+SOURCES = ["vj_capi.hip", "vj_gemm.hip", "vj_gemm256.hip", "vj_attn.hip", "vj_ops.hip", "vj_f32.hip", "vj_xattn.hip", "vj_variants.hip"]
 ARCH = os.environ.get("VJEPA_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -amdgpu-mfma-vgpr-form: MFMA accumulators in arch VGPRs (gfx950 allows it), so the softmax /

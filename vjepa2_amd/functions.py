@@ -189,6 +189,8 @@ def block_forward_fp8(x, blk, lay):
     scaled e4m3; attention, proj and fc2 stay bf16 (their inputs come out of the attention / GELU
     kernels, whose rows span many tiles). f32 residual stream as in block_forward."""
     attn, mlp = blk.attn, blk.mlp
+    if getattr(mlp, "swiglu", False) or _drop_scales(blk, lay, x.device) is not None:
+        raise NotImplementedError("the fp8 block path covers the GELU MLP without drop_path")
     H = attn.num_heads
     hd = x.shape[1] // H
     ln1, e1 = ops.layernorm_fwd_fp8(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps)
@@ -206,12 +208,51 @@ def block_forward_fp8(x, blk, lay):
     return ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, _resid_epi(x), resid=x_mid)
 
 
+def _drop_scales(blk, lay, device):
+    """Stochastic depth (Block.forward, modules.py:561-562: timm drop_path(x, drop_prob, training)):
+    per-row factors (attention branch, MLP branch) — each sequence's draw repeated over its tokens —
+    or None when the block has no active DropPath. Draw order per block as in the reference: the
+    attention branch's, then the MLP branch's."""
+    dp = blk.drop_path
+    if not getattr(dp, "drop_prob", None) or not dp.training:
+        return None
+    lens = torch.tensor([ln for n, ln in lay.groups for _ in range(n)], device=device)
+    return tuple(dp.sample(lens.numel(), device).repeat_interleave(lens, output_size=lay.T) for _ in range(2))
+
+
+def _branch_out(inp, lin, resid, scale):
+    """resid + lin(inp): the residual add of a branch, fused into the output GEMM's epilogue; with a
+    drop_path factor the GEMM writes the branch and vj_rowscale_add scales and adds it."""
+    if scale is None:
+        return ops.linear_fwd(inp, weight_bf16(lin.weight), lin.bias, _resid_epi(resid), resid=resid)
+    return ops.rowscale_add(ops.linear_fwd(inp, weight_bf16(lin.weight), lin.bias, EPI_F32), scale, resid)
+
+
+def _mlp_forward(ln2, mlp, save):
+    """The MLP up to its output projection: (that projection's input, the output Linear, saved).
+    GELU MLP (modules.py:77-83): fc1 + GELU in one GEMM epilogue, which also saves GELU'(pre-activation)
+    for the backward (bf16, the bytes the pre-activation took). SwiGLUFFN (modules.py:102-106): fc1 and
+    fc2 write x1 | x2 side by side, vj_swiglu_fwd makes silu(x1) * x2."""
+    T = ln2.shape[0]
+    if getattr(mlp, "swiglu", False):
+        h = mlp.fc1.weight.shape[0]
+        x12 = torch.empty(T, 2 * h, dtype=BF16, device=ln2.device)
+        ops.linear_fwd(ln2, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_BF16, out=x12[:, :h])
+        ops.linear_fwd(ln2, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_BF16, out=x12[:, h:])
+        hidden = ops.swiglu_fwd(x12)
+        return hidden, mlp.fc3, ((x12, hidden) if save else None)
+    dgelu = torch.empty(T, mlp.fc1.weight.shape[0], dtype=BF16, device=ln2.device) if save else None
+    _, act = ops.linear_fwd(ln2, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=dgelu)
+    return act, mlp.fc2, ((dgelu, act) if save else None)
+
+
 def block_forward(x, blk, lay, save):
     T, D = x.shape
     assert not (save and x.dtype == BF16), "the training path keeps the residual stream in f32"
     attn, mlp = blk.attn, blk.mlp
     H = attn.num_heads
     hd = D // H
+    scales = _drop_scales(blk, lay, x.device)
     ln1, m1, r1 = ops.layernorm_fwd(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, want_stats=save)
     if attn.use_rope:  # QKV GEMM with RoPE of q, k fused into its epilogue
         c, s = rope_tables(hd, x.device, lay.npos)
@@ -220,14 +261,11 @@ def block_forward(x, blk, lay, save):
     else:
         qkv = ops.linear_fwd(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
     o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd, lay), fblk=lay.fblk)
-    x_mid = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, _resid_epi(x), resid=x)
+    x_mid = _branch_out(o, attn.proj, x, scales and scales[0])
     ln2, m2, r2 = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, want_stats=save)
-    hidden = mlp.fc1.weight.shape[0]
-    # the fc1 epilogue saves GELU'(pre-activation) for the backward (bf16, the bytes the pre-activation took)
-    dgelu = torch.empty(T, hidden, dtype=BF16, device=x.device) if save else None
-    _, act = ops.linear_fwd(ln2, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=dgelu)
-    x_out = ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, _resid_epi(x), resid=x_mid)
-    saved = (x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, dgelu, act) if save else None
+    hidden, out_lin, msaved = _mlp_forward(ln2, mlp, save)
+    x_out = _branch_out(hidden, out_lin, x_mid, scales and scales[1])
+    saved = (x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, msaved, scales) if save else None
     return x_out, saved
 
 
@@ -236,6 +274,8 @@ def block_forward_f32(x, blk, lay):
     (vj_gemm_f32) and exact-softmax attention (vj_attn_fwd_f32); every intermediate stays f32."""
     if lay.fblk:
         raise NotImplementedError("the fp32-operand parity mode has no frame-causal attention")
+    if getattr(blk.mlp, "swiglu", False) or _drop_scales(blk, lay, x.device) is not None:
+        raise NotImplementedError("the fp32-operand parity mode covers the GELU MLP without drop_path")
     attn, mlp = blk.attn, blk.mlp
     H = attn.num_heads
     hd = x.shape[1] // H
@@ -354,27 +394,62 @@ def _ln_grads(ln):
     return grad_buf(ln.weight), grad_buf(ln.bias)
 
 
-def block_backward(dxo, blk, lay, saved):
-    x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, dgelu, act = saved
-    attn, mlp = blk.attn, blk.mlp
-    T, D = x.shape
-    H = attn.num_heads
-    hd = D // H
-    twin = getattr(dxo, "_vj_grad_bf16", None)  # bf16 twin written by the next block's LN1 backward,
-    dxo_b = twin[0] if twin is not None and twin[1] == dxo._version else ops.cast_bf16(dxo)  # unless changed since
-    # MLP (each weight gradient is issued before the data gradient that shares its dY, so on the
-    # weight-gradient stream the two overlap)
-    with _OnWgradStream(dxo_b, act):
-        wgrad(dxo_b, act, mlp.fc2.weight)  # fc2 bias grad: fused into LN2 backward
-    dpre = ops.linear_dgrad(dxo_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
+def _mlp_backward(dy_b, mlp, ln2, saved):
+    """bf16 gradient of the MLP output -> bf16 gradient of its input ln2; weight and hidden-bias
+    gradients accumulated (the output Linear's bias gradient is the caller's). Each weight gradient is
+    issued before the data gradient that shares its dY, so on the weight-gradient stream the two overlap.
+    SwiGLU: d(ln2) = dx1 W1 + dx2 W2, the second dgrad GEMM adding the first's output in its epilogue
+    (autograd sums the two Linears' input gradients)."""
+    if getattr(mlp, "swiglu", False):
+        x12, hidden = saved
+        h = hidden.shape[1]
+        with _OnWgradStream(dy_b, hidden):
+            wgrad(dy_b, hidden, mlp.fc3.weight)
+        dh = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc3.weight), wt=weight_bf16_t(mlp.fc3.weight))
+        dx12 = ops.swiglu_bwd(dh, x12)
+        dx1, dx2 = dx12[:, :h], dx12[:, h:]
+        with _OnWgradStream(dx12, ln2):
+            wgrad(dx1, ln2, mlp.fc1.weight)
+            _bias_grad(mlp.fc1, dx1)
+            wgrad(dx2, ln2, mlp.fc2.weight)
+            _bias_grad(mlp.fc2, dx2)
+        dl = ops.linear_dgrad(dx1, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
+        return ops.linear_dgrad(dx2, weight_bf16(mlp.fc2.weight), wt=weight_bf16_t(mlp.fc2.weight), resid=dl)
+    dgelu, act = saved
+    with _OnWgradStream(dy_b, act):
+        wgrad(dy_b, act, mlp.fc2.weight)
+    dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
     with _OnWgradStream(dpre, ln2):
         wgrad(dpre, ln2, mlp.fc1.weight)
         _bias_grad(mlp.fc1, dpre)
-    dln2 = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
+    return ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
+
+
+def block_backward(dxo, blk, lay, saved):
+    x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, msaved, scales = saved
+    attn, mlp = blk.attn, blk.mlp
+    out_lin = mlp.fc3 if getattr(mlp, "swiglu", False) else mlp.fc2
+    T, D = x.shape
+    H = attn.num_heads
+    hd = D // H
+    if scales is None:
+        twin = getattr(dxo, "_vj_grad_bf16", None)  # bf16 twin written by the next block's LN1 backward,
+        dy_mlp = twin[0] if twin is not None and twin[1] == dxo._version else ops.cast_bf16(dxo)  # unless changed
+    else:  # drop_path: the MLP branch's dY = its factor x dxo (bias gradient from it, not from dxo)
+        dy_mlp = ops.rowscale_bf16(dxo, scales[1])
+        _bias_grad(out_lin, dy_mlp)
+    dln2 = _mlp_backward(dy_mlp, mlp, ln2, msaved)
     gw, gb = _ln_grads(blk.norm2)
+    # without drop_path the output-projection / proj bias gradients are the column sums of dxo / dxm,
+    # fused into the LayerNorm backward
+    fused = scales is None
     dxm, dxm_b = ops.layernorm_bwd(dln2, x_mid, m2, r2, blk.norm2.weight, dres_in=dxo, dweight=gw, dbias=gb,
-                                   want_bf16=True, sum_in=_bias_buf(mlp.fc2), sum_out=_bias_buf(attn.proj))
-    # attention (proj bias grad = column sums of dxm, produced above)
+                                   want_bf16=fused, sum_in=_bias_buf(out_lin) if fused else None,
+                                   sum_out=_bias_buf(attn.proj) if fused else None)
+    if not fused:
+        dxm_b = ops.rowscale_bf16(dxm, scales[0])
+        _bias_grad(attn.proj, dxm_b)
+    # attention
     with _OnWgradStream(dxm_b, o):
         wgrad(dxm_b, o, attn.proj.weight)
     do = ops.linear_dgrad(dxm_b, weight_bf16(attn.proj.weight), wt=weight_bf16_t(attn.proj.weight))
@@ -470,23 +545,16 @@ def attn_module_backward(dy, attn, lay, saved):
 
 
 def mlp_module_forward(x, mlp):
-    """x bf16 [T, C] -> (fc2(GELU(fc1 x)) f32, saved)."""
-    T = x.shape[0]
-    dgelu = torch.empty(T, mlp.fc1.weight.shape[0], dtype=BF16, device=x.device)
-    _, act = ops.linear_fwd(x, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=dgelu)
-    y = ops.linear_fwd(act, weight_bf16(mlp.fc2.weight), mlp.fc2.bias, EPI_F32)
-    return y, (x, dgelu, act)
+    """x bf16 [T, C] -> (fc2(GELU(fc1 x)) or SwiGLU's fc3(silu(fc1 x) * fc2 x), f32; saved)."""
+    hidden, out_lin, msaved = _mlp_forward(x, mlp, True)
+    y = ops.linear_fwd(hidden, weight_bf16(out_lin.weight), out_lin.bias, EPI_F32)
+    return y, (x, msaved)
 
 
 def mlp_module_backward(dy, mlp, saved):
-    x, dgelu, act = saved
-    dy_b = ops.cast_bf16(dy)
-    dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
-    wgrad(dy_b, act, mlp.fc2.weight)
-    _bias_grad(mlp.fc2, dy)
-    dx = ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
-    wgrad(dpre, x, mlp.fc1.weight)
-    _bias_grad(mlp.fc1, dpre)
+    x, msaved = saved
+    dx = _mlp_backward(ops.cast_bf16(dy), mlp, x, msaved)
+    _bias_grad(mlp.fc3 if getattr(mlp, "swiglu", False) else mlp.fc2, dy)
     return dx
 
 

@@ -37,6 +37,64 @@ class MLP(nn.Module):
         return y.reshape(*shp[:-1], y.shape[-1])
 
 
+class SwiGLUFFN(nn.Module):
+    """modules.py:86-106 (act_layer=nn.SiLU): fc1, fc2: in -> h (h = hidden rounded as 2/3 hidden up to a
+    multiple of 8 when wide_silu), fc3: h -> out; fc3(silu(fc1 x) * fc2 x). `drop` is accepted and unused,
+    as in the reference."""
+
+    swiglu = True
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.SiLU, drop=0.0,
+                 wide_silu=True):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden = hidden_features or in_features
+        if wide_silu:
+            hidden = (int(2 * hidden / 3) + 7) // 8 * 8
+        self.fc1 = nn.Linear(in_features, hidden)
+        self.fc2 = nn.Linear(in_features, hidden)
+        self.act = act_layer()
+        self.fc3 = nn.Linear(hidden, out_features)
+        if act_layer is not nn.SiLU:
+            raise NotImplementedError("SwiGLUFFN gates with SiLU (the reference builds it for act_layer=nn.SiLU)")
+        if hidden % 8:
+            raise NotImplementedError(f"SwiGLU hidden width {hidden} is not a multiple of 8 (16-B GEMM rows)")
+
+    def forward(self, x):
+        """fc1 / fc2 GEMMs side by side, vj_swiglu_fwd gate, fc3 (f32 out)."""
+        shp = x.shape
+        y = fn.run_sublayer(x.reshape(-1, shp[-1]), self)
+        return y.reshape(*shp[:-1], y.shape[-1])
+
+
+class DropPath(nn.Module):
+    """modules.py:53-64: stochastic depth, timm's drop_path (timm 0.9.x, not in this image; restated):
+    in training, a residual branch's output is multiplied per sample by Bernoulli(keep) / keep
+    (keep = 1 - drop_prob), drawn as x.new_empty((B, 1, 1)).bernoulli_(keep).div_(keep) in the branch's
+    dtype (bf16 under autocast). It runs fused in Block / ACBlock (functions.block_forward draws one
+    factor per sequence and branch with sample(), the kernels scale the branch rows)."""
+
+    def __init__(self, drop_prob=None):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def sample(self, n, device):
+        """n per-sample factors (f32 holding the bf16 values the reference's random_tensor takes)."""
+        keep = 1.0 - self.drop_prob
+        rt = torch.empty(n, dtype=torch.bfloat16, device=device).bernoulli_(keep)
+        if keep > 0.0:
+            rt.div_(keep)
+        return rt.float()
+
+    def forward(self, x):
+        if not self.drop_prob or not self.training:
+            return x
+        raise NotImplementedError("DropPath runs fused inside Block / ACBlock (functions.block_forward)")
+
+    def extra_repr(self):
+        return f"p={self.drop_prob}"
+
+
 class RoPEAttention(nn.Module):
     """modules.py:261-382: fused QKV, 3-axis RoPE on the (frame, row, col) of each token id, SDPA."""
 
@@ -107,8 +165,15 @@ def _check_attn(head_dim, attn_drop, proj_drop, is_causal):
         raise NotImplementedError("causal attention is not on the V-JEPA pre-training path")
 
 
+def _make_mlp(dim, hidden, act_layer, wide_silu, drop):
+    """Block's MLP choice (modules.py:548-554): SwiGLUFFN for nn.SiLU, else the GELU MLP."""
+    if act_layer is nn.SiLU:
+        return SwiGLUFFN(in_features=dim, hidden_features=hidden, act_layer=act_layer, wide_silu=wide_silu, drop=drop)
+    return MLP(in_features=dim, hidden_features=hidden, act_layer=act_layer, drop=drop)
+
+
 class Block(nn.Module):
-    """modules.py:500-563: x = x + attn(norm1(x)); x = x + mlp(norm2(x))."""
+    """modules.py:500-563: x = x + drop_path(attn(norm1(x))); x = x + drop_path(mlp(norm2(x)))."""
 
     def __init__(self, dim, num_heads, mlp_ratio=4.0, qkv_bias=False, qk_scale=None, drop=0.0, attn_drop=0.0,
                  drop_path=0.0, act_layer=nn.GELU, wide_silu=True, norm_layer=nn.LayerNorm, use_sdpa=True,
@@ -122,14 +187,9 @@ class Block(nn.Module):
         else:
             self.attn = Attention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
                                   attn_drop=attn_drop, use_sdpa=use_sdpa, is_causal=is_causal, proj_drop=drop)
-        if drop_path > 0.0:
-            raise NotImplementedError("stochastic depth (drop_path > 0) is not implemented (configs use 0)")
-        self.drop_path = nn.Identity()
+        self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
         self.norm2 = norm_layer(dim)
-        mlp_hidden_dim = int(dim * mlp_ratio)
-        if act_layer is nn.SiLU:
-            raise NotImplementedError("SwiGLU MLP (use_silu) is not implemented on the HIP path (configs use GELU)")
-        self.mlp = MLP(in_features=dim, hidden_features=mlp_hidden_dim, act_layer=act_layer, drop=drop)
+        self.mlp = _make_mlp(dim, int(dim * mlp_ratio), act_layer, wide_silu, drop)
 
     def layout_for(self, B, N, mask, T, H_patches, W_patches, device):
         g = self.attn.grid_size if self.attn.use_rope else 1
@@ -211,13 +271,9 @@ class ACBlock(nn.Module):
         else:
             self.attn = Attention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
                                   attn_drop=attn_drop, use_sdpa=use_sdpa, is_causal=is_causal, proj_drop=drop)
-        if drop_path > 0.0:
-            raise NotImplementedError("stochastic depth (drop_path > 0) is not implemented (configs use 0)")
-        self.drop_path = nn.Identity()
+        self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
         self.norm2 = norm_layer(dim)
-        if act_layer is nn.SiLU:
-            raise NotImplementedError("SwiGLU MLP (use_silu) is not implemented on the HIP path (configs use GELU)")
-        self.mlp = MLP(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
+        self.mlp = _make_mlp(dim, int(dim * mlp_ratio), act_layer, wide_silu, drop)
 
     def forward(self, x, mask=None, attn_mask=None, T=None, H=None, W=None, action_tokens=0):
         if mask is not None:

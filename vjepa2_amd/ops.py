@@ -157,9 +157,18 @@ def linear_fwd(x, w, bias=None, epi=EPI_BF16, out=None, out2=None, resid=None):
     return (out, out2) if epi == EPI_GELU else out
 
 
-def linear_dgrad(dy, w, out=None, gelu_grad=None, wt=None):
+def linear_dgrad(dy, w, out=None, gelu_grad=None, wt=None, resid=None):
     """dX = dY W (bf16 out); with gelu_grad (the GELU derivative the forward's EPI_GELU saved): dX = (dY W) * gelu_grad. `wt` = W^T [K, N] contiguous (the
-    K-major B operand the paired GEMM reads); without it W is read MN-major (256-row kernel)."""
+    K-major B operand the paired GEMM reads); without it W is read MN-major (256-row kernel).
+    resid (bf16 [M, K], needs wt): dX = resid + dY W (the gradient of an input read by two Linears)."""
+    if resid is not None:
+        M, K = dy.shape[0], w.shape[1]
+        assert gelu_grad is None and wt is not None and resid.dtype == BF16 and resid.shape == (M, K)
+        assert dy.shape[1] % 8 == 0 and K % 8 == 0
+        out = out if out is not None else torch.empty(M, K, dtype=BF16, device=dy.device)
+        gemm(M, K, dy.shape[1], dy, _rowmajor(dy, "dy"), True, wt, _rowmajor(wt, "wt"), True, EPI_BF16_RESID, out=out,
+             ldc=out.stride(0), aux=resid, ldaux=_rowmajor(resid, "resid"))
+        return out
     M, N = dy.shape
     K = w.shape[1]
     assert w.shape[0] == N
@@ -256,6 +265,51 @@ def linear_wgrad(dy, x, dw, accumulate=True):
         gemm(N, K, M, dy, _rowmajor(dy, "dy"), False, x, _rowmajor(x, "x"), False, EPI_F32, out=dw,
              ldc=dw.stride(0), splitk=wgrad_splitk(N, K, M))
     return dw
+
+
+# ------------------------------------------------------------------------------------------------
+# Block variants (vj_variants.hip): SwiGLU gate and drop_path row scaling
+def swiglu_fwd(x12, out=None):
+    """x12 bf16 [M, 2h] = fc1(x) | fc2(x) -> bf16 [M, h] = silu(x1) * x2 (SwiGLUFFN, modules.py:102-106)."""
+    _dev(x12, out)
+    assert x12.dtype == BF16 and x12.shape[1] % 2 == 0
+    M, h = x12.shape[0], x12.shape[1] // 2
+    out = out if out is not None else torch.empty(M, h, dtype=BF16, device=x12.device)
+    _call("vj_swiglu_fwd", M, h, _p(x12), _rowmajor(x12, "x12"), _p(out), _rowmajor(out, "out"), _stream())
+    return out
+
+
+def swiglu_bwd(dh, x12, out=None):
+    """dh bf16 [M, h], x12 (the forward's fc1 | fc2 outputs) -> dx12 bf16 [M, 2h] = dx1 | dx2."""
+    _dev(dh, x12, out)
+    M, h = dh.shape
+    assert dh.dtype == BF16 and x12.dtype == BF16 and x12.shape == (M, 2 * h)
+    out = out if out is not None else torch.empty(M, 2 * h, dtype=BF16, device=dh.device)
+    _call("vj_swiglu_bwd", M, h, _p(dh), _rowmajor(dh, "dh"), _p(x12), _rowmajor(x12, "x12"), _p(out),
+          _rowmajor(out, "out"), _stream())
+    return out
+
+
+def rowscale_add(y, scale, resid, out=None):
+    """resid + bf16(bf16(y) * scale[row]) (drop_path on a residual branch): y f32 [M, N], scale f32 [M],
+    resid f32 or bf16 [M, N] (out in resid's dtype)."""
+    _dev(y, scale, resid, out)
+    M, N = y.shape
+    assert y.dtype == F32 and scale.dtype == F32 and scale.numel() == M and resid.shape == (M, N)
+    out = out if out is not None else torch.empty_like(resid)
+    _call("vj_rowscale_add", M, N, _p(y), _rowmajor(y, "y"), _p(scale), _p(resid), _rowmajor(resid, "resid"), _p(out),
+          _rowmajor(out, "out"), int(resid.dtype == BF16), _stream())
+    return out
+
+
+def rowscale_bf16(dx, scale, out=None):
+    """bf16(bf16(dx) * scale[row]): dx f32 [M, N] -> bf16 [M, N] (drop_path's backward)."""
+    _dev(dx, scale, out)
+    M, N = dx.shape
+    assert dx.dtype == F32 and scale.dtype == F32 and scale.numel() == M
+    out = out if out is not None else torch.empty(M, N, dtype=BF16, device=dx.device)
+    _call("vj_rowscale_bf16", M, N, _p(dx), _rowmajor(dx, "dx"), _p(scale), _p(out), _rowmajor(out, "out"), _stream())
+    return out
 
 
 # ------------------------------------------------------------------------------------------------

@@ -15,6 +15,7 @@ oracle (oracle/vjepa_oracle.py, fp32) on a bounded sample of the same workload.
 """
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -40,6 +41,21 @@ MODELS = {"vit_large": dict(D=1024, depth=24, heads=16, mlp=4096), "vit_small": 
           "vit_huge": dict(D=1280, depth=32, heads=16, mlp=5120),
           "vit_giant": dict(D=1408, depth=40, heads=16, mlp=6144),
           "vit_giant_xformers": dict(D=1408, depth=40, heads=22, mlp=6144)}
+
+
+@contextlib.contextmanager
+def _serialised():
+    """Both side streams off (VJ_TGT_STREAM=0, VJ_WGRAD_STREAM=0) for the enclosed steps."""
+    old = {e: os.environ.get(e) for e in ("VJ_TGT_STREAM", "VJ_WGRAD_STREAM")}
+    os.environ.update({e: "0" for e in old})
+    try:
+        yield
+    finally:
+        for e, v in old.items():
+            if v is None:
+                os.environ.pop(e, None)
+            else:
+                os.environ[e] = v
 
 
 def step_flops(model, B, N, masks_enc, masks_pred, pd=384, pdepth=12, pmlp=1536, kdim=1536):
@@ -137,15 +153,21 @@ def main():
     # Per-launch breakdown from the last (untimed) warmup step: a HIP event pair around every one of
     # its ~1500 launches. Inside the timed region only the dominant kernel's launches carry events
     # (the roofline's live average), so the timing is not inflated by the breakdown.
+    # That step runs SERIALISED (target-encoder and weight-gradient side streams off): with the streams
+    # on, concurrent kernels share the CUs and every per-launch time (events or rocprof) includes the
+    # other stream's work, so neither the per-kernel rooflines nor the choice of the dominant kernel
+    # would describe the kernels themselves.
     breakdown = None
     for i in range(args.warmup):
         full = ops.KernelEvents() if (args.kernel_events and i == args.warmup - 1) else None
         if full:
-            full.start()
-        run(i)
-        if full:
-            full.stop()
+            with _serialised():
+                full.start()
+                run(i)
+                full.stop()
             breakdown = full.summary()
+        else:
+            run(i)
     torch.cuda.synchronize()
 
     dominant = max(breakdown, key=lambda k: breakdown[k]["total_ms"]) if breakdown else None
@@ -213,24 +235,26 @@ def main():
             roof["traffic_unit"] = "B/launch"
             roof["traffic_source"] = tr["source"]
 
-    # By default (VJ_TGT_STREAM unset or 1) the target encoder's forward runs on a side stream
-    # (train.py), so inside the timed region the dominant kernel shares the CUs with it. One more
-    # UNTIMED step with the side stream off then gives the same kernel's unshared launch duration.
-    if roof and os.environ.get("VJ_TGT_STREAM", "1") == "1":
+    # By default the target encoder's forward and the backward's weight-gradient GEMMs run on side
+    # streams (train.py, functions.py), so inside the timed region the dominant kernel shares the CUs
+    # with them. One more UNTIMED step with both streams off gives the same kernel's unshared launch
+    # duration (what the serialised rocprofv3 profile under profiles/ shows).
+    shared = [n for n, e, d in (("target-encoder side stream", "VJ_TGT_STREAM", "1"),
+                                ("weight-gradient stream", "VJ_WGRAD_STREAM", "1")) if os.environ.get(e, d) == "1"]
+    if roof and shared:
         solo = ops.KernelEvents(only={dom})
-        os.environ["VJ_TGT_STREAM"] = "0"
         torch.cuda.synchronize()
-        solo.start()
-        run(nsteps - 1)
-        solo.stop()
+        with _serialised():
+            solo.start()
+            run(nsteps - 1)
+            solo.stop()
         torch.cuda.synchronize()
-        os.environ["VJ_TGT_STREAM"] = "1"
         st1 = solo.summary()[dom]
         a1 = st1["flops"] / (st1["total_ms"] * 1e-3) / 1e12
-        roof["timed_region_shares_cus_with"] = "target-encoder side stream"
+        roof["timed_region_shares_cus_with"] = " and ".join(shared)
         roof["unshared"] = {"achieved": round(a1, 1), "frac": round(a1 / PEAK_BF16_TFLOPS, 4),
                             "avg_launch_us": round(st1["total_ms"] * 1e3 / st1["count"], 2),
-                            "measured": "one extra untimed step, target encoder on the main stream"}
+                            "measured": "one extra untimed step with both side streams off"}
 
     # Untimed comparison (not the headline): the same steps with the reference loop's per-step host
     # sync (float(loss) every iteration, app/vjepa/train.py:468), to state what the free-running

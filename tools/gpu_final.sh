@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-me
 rc=$?; echo "pytest rc=$rc"; tail -3 "$out/pytest.log"; [ $rc -ge 2 ] && exit $rc
 timeout -k 10 300 python -u bench.py > "$out/bench.log" 2>&1 || { echo "bench failed"; tail -5 "$out/bench.log"; exit 3; }
 tail -c 600 "$out/bench.log"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --kernel-events 0 --synced-steps 0 > "$out/prof.log" 2>&1 || { echo "prof failed"; tail -5 "$out/prof.log"; exit 4; }
+VJ_TGT_STREAM=0 VJ_WGRAD_STREAM=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --kernel-events 0 --synced-steps 0 > "$out/prof.log" 2>&1 || { echo "prof failed"; tail -5 "$out/prof.log"; exit 4; }
 echo "prof ok"
 bash tools/pmc_bench.sh "$tag" > "$out/pmc.log" 2>&1 || { echo "pmc failed"; tail -5 "$out/pmc.log"; exit 5; }
 echo "pmc ok"

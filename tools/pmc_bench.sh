@@ -11,7 +11,7 @@ passes=("SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
 i=0
 for p in "${passes[@]}"; do
   i=$((i + 1))
-  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $p -d "$out/p$i" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 --kernel-events 0 --synced-steps 0 "$@" > "$out/p$i.log" 2>&1
+  VJ_TGT_STREAM=0 VJ_WGRAD_STREAM=0 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $p -d "$out/p$i" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 --kernel-events 0 --synced-steps 0 "$@" > "$out/p$i.log" 2>&1
   rc=$?
   echo "pass $i ($p) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$out/p$i.log"; exit $rc; fi

@@ -21,12 +21,13 @@ EPI = {"EPI_BF16": 0, "EPI_F32": 1, "EPI_F32_RESID": 2, "EPI_GELU": 3, "EPI_GELU
 
 
 def name_regex(label):
-    m = re.fullmatch(r"k_gemm<(\d),(\d),(\w+)>", label)
+    m = re.fullmatch(r"k_gemm<(\d),(\d),(\w+)>(\[splitk\])?", label)
     if m:
         b = {"1": "true", "0": "false"}
+        epi = EPI["EPI_PARTIAL"] if m[4] else EPI[m[3]]  # split-K slices write f32 partial slabs
         # every tile width, the 8-wave, two-workgroups-per-CU (", false, 4"), 192-row and staggered
         # (trailing ", true") instantiations
-        return re.compile(rf"k_gemm256<{b[m[1]]}, {b[m[2]]}, {EPI[m[3]]}, \d+(, (?:true|false|\d+))*>")
+        return re.compile(rf"k_gemm256<{b[m[1]]}, {b[m[2]]}, {epi}, \d+(, (?:true|false|\d+))*>")
     return re.compile(re.escape(label.split("<")[0]) + r"\b")
 
 

@@ -107,11 +107,16 @@ def gemm(M, N, K, a, lda, a_kmajor, b, ldb, b_kmajor, epi, out=None, ldc=0, out2
           _p(out), ldc, _p(out2), ldc2, _stream(), label=label, flops=2.0 * M * N * K)
 
 
-def wgrad_splitk(M, N, K, cus=256):
+def wgrad_splitk(M, N, K, cus=None):
     """Split K (tokens) of a weight-gradient GEMM [M, N] += A[M, K] B[K, N]. Tiles are 256 x (256 or
     128) when M >= 256 and N >= 128 (the C side's choice), else 128 x 128. Picks the split that
     minimises (waves of tiles on the CUs) x (work per tile) + the f32 partial-slab traffic, keeping
-    >= 512 of K per slice."""
+    >= 512 of K per slice. `cus`: the CUs the GEMM is sized for — half the chip when the weight
+    gradients run on their own stream beside the data-gradient chain (functions.wgrad_stream: fewer
+    slices, less slab traffic; +0.3 % clips/s / +0.8 % median step over 5 interleaved bench runs
+    against sizing for all 256, profiles/r04_wgrad_split_step_ab.txt), the whole chip otherwise."""
+    if cus is None:
+        cus = 128 if os.environ.get("VJ_WGRAD_STREAM", "1") == "1" else 256
     if M >= 256 and N >= 128:
         tm, tn, per_cu = 256, (256 if N % 256 == 0 else 128), 1
     else:

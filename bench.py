@@ -130,6 +130,9 @@ def main():
                                        mixed_precision=True)
     trainer = JEPATrainer(enc, pred, tgt, opt, mixed_precision=True, loss_exp=1.0, world_size=world,
                           fp8_target=bool(args.fp8_target))
+    # every step's clips and masks are on the device before the first step (below): the next step's
+    # target forward may start under the previous step's staged update (JEPATrainer.apply_update)
+    trainer.inputs_resident = os.environ.get("VJ_STAGED_UPDATE", "1") == "1"
 
     # inputs resident in HBM before timing: clips + masks for every step (dataloader prefetch)
     torch.manual_seed(239 + rank)

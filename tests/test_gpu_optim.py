@@ -204,3 +204,48 @@ def test_lazy_zero_overwrite_marked_grad_not_written_is_zero():
     torch.cuda.synchronize()
     for p, r in zip(ps, ref):
         torch.testing.assert_close(p.detach().cpu(), r.detach(), rtol=2e-6, atol=2e-7)
+
+
+def test_staged_update_matches_one_pass():
+    """The staged AdamW + EMA issue (JEPATrainer.inputs_resident: the next step's target forward waits
+    per stage on the side stream) gives bitwise the losses, parameters and target weights of the
+    one-pass update over 3 steps."""
+    import copy
+
+    from vjepa2_amd.masks import MaskCollator
+    from vjepa2_amd.train import JEPATrainer, init_opt, init_video_model
+
+    dev = torch.device("cuda", 0)
+    T, S, B = 8, 64, 2
+    masks = [dict(aspect_ratio=[0.75, 1.5], num_blocks=8, spatial_scale=[0.15, 0.15], temporal_scale=[1.0, 1.0]),
+             dict(aspect_ratio=[0.75, 1.5], num_blocks=2, spatial_scale=[0.7, 0.7], temporal_scale=[1.0, 1.0])]
+    torch.manual_seed(0)
+    mc = MaskCollator(masks, [T], crop_size=S, patch_size=16)
+    data = []
+    for i in range(3):
+        (_, me, mp), = mc([(0, 0, [torch.arange(T)])] * B)
+        clips = torch.randn(B, 3, T, S, S, generator=torch.Generator().manual_seed(i)).to(dev)
+        data.append(([clips], [[m.to(dev) for m in me]], [[m.to(dev) for m in mp]]))
+    torch.cuda.synchronize()
+
+    def run(staged):
+        torch.manual_seed(239)
+        enc, pred = init_video_model(device=dev, patch_size=16, max_num_frames=T, tubelet_size=2,
+                                     model_name="vit_small", crop_size=S, pred_depth=2, pred_num_heads=12,
+                                     pred_embed_dim=384, uniform_power=True, use_mask_tokens=True, num_mask_tokens=2,
+                                     use_sdpa=True, use_rope=True)
+        tgt = copy.deepcopy(enc)
+        opt, _, _, _ = init_opt(enc, pred, iterations_per_epoch=10, start_lr=1e-4, ref_lr=1e-4, warmup=0,
+                                num_epochs=1, wd=0.04, final_wd=0.04, mixed_precision=True)
+        tr = JEPATrainer(enc, pred, tgt, opt, mixed_precision=True)
+        tr.inputs_resident = staged
+        losses = [tr.train_step(c, me, mp, 0.99).clone() for c, me, mp in data]
+        assert (tr._staged is not None) == staged  # the last step staged its update (unused yet)
+        torch.cuda.synchronize()
+        return ([l.item() for l in losses], [a.data.clone() for a in tr.opt.arenas],
+                [a.data.clone() for a in tr.tgt_arenas])
+
+    a, b = run(False), run(True)
+    assert a[0] == b[0]
+    for x, y in zip(a[1] + a[2], b[1] + b[2]):
+        assert torch.equal(x, y)

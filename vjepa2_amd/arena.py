@@ -188,30 +188,42 @@ class FusedAdamW:
                 self.pstep[i][idx] -= 1
         self._pending = None
 
-    def step(self, grad_scale=1.0, found_inf=None, exclude=(), ema=None):
+    def step(self, grad_scale=1.0, found_inf=None, exclude=(), ema=None, stages=None):
         """One AdamW step over every arena. ema = (targets, momentum), targets[i] the target arena of
         arena i (same layout) or None: the EMA of train.py:456-465 is fused into the AdamW pass of that
         arena (the online parameters are read once); an arena with excluded parameters gets the plain
-        EMA after its AdamW instead."""
+        EMA after its AdamW instead.
+
+        stages: optional list of parameter lists in the order the next forward uses them (e.g. patch
+        embedding, block 0, block 1, ...): the update is issued stage by stage (every arena's slice of a
+        stage, then the next stage) and a HIP event is recorded on the current stream after each;
+        returns those events (parameters in no stage form a last stage). Each stage's parameters must be
+        consecutive in every arena (they are: arenas hold named_parameters() order reversed). Without
+        stages: one pass per arena (None returned)."""
         self._resolve()
         for a in self.arenas:
             a.finalize_grads()
         ex = {id(p) for p in exclude}
         advanced = []
         late_ema = []
+        work = []  # per arena: (arena index, active mask, fuse, target arena)
         for i, (g, a) in enumerate(zip(self.param_groups, self.arenas)):
             act = np.array([id(p) not in ex for p in a.params], dtype=bool)
             st = self.pstep[i]
             st[act] += 1
             advanced.append((i, np.nonzero(act)[0]))
-            b1, b2 = g["betas"]
-            wd = 0.0 if g.get("WD_exclude", False) else g["weight_decay"]
             tgt = ema[0][i] if ema is not None else None
             fuse = tgt is not None and bool(act.all()) and tgt.numel == a.numel
             if tgt is not None and not fuse:
                 late_ema.append((tgt, a))
-            j, n = 0, len(a.params)
-            while j < n:  # maximal runs of active params with equal step count (they tile the arena when all are active)
+            work.append((i, act, fuse, tgt))
+
+        def run(i, act, fuse, tgt, j, n):
+            # maximal runs of active params with equal step count in params [j, n) of arena i
+            g, a, st = self.param_groups[i], self.arenas[i], self.pstep[i]
+            b1, b2 = g["betas"]
+            wd = 0.0 if g.get("WD_exclude", False) else g["weight_decay"]
+            while j < n:
                 if not act[j]:
                     j += 1
                     continue
@@ -227,6 +239,21 @@ class FusedAdamW:
                     ops.adamw(a.data[lo:hi], a.grad[lo:hi], a.exp_avg[lo:hi], a.exp_avg_sq[lo:hi], a.bf16[lo:hi],
                               g["lr"], b1, b2, g["eps"], wd, int(st[j]), grad_scale=grad_scale, found_inf=found_inf)
                 j = k
+
+        events = None
+        if stages is None:
+            for i, act, fuse, tgt in work:
+                run(i, act, fuse, tgt, 0, len(act))
+        else:
+            events = []
+            ranges = self._stage_ranges(stages)
+            for s in range(len(ranges)):
+                for i, act, fuse, tgt in work:
+                    j, n = ranges[s][i]
+                    run(i, act, fuse, tgt, j, n)
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
         for t, a in late_ema:
             ops.ema(t.data, a.data, ema[1], t.bf16)
         SHADOW_EPOCH[0] += 1  # the bf16 shadows changed: cached W^T copies are stale
@@ -236,6 +263,30 @@ class FusedAdamW:
             ev = torch.cuda.Event()
             ev.record()
             self._pending = (flag, ev, advanced)
+        return events
+
+    def _stage_ranges(self, stages):
+        """Per stage, per arena: the [j0, j1) parameter-index range of the stage's parameters
+        (empty (0, 0) when the arena holds none); cached per stage list."""
+        key = tuple(tuple(id(p) for p in st) for st in stages)
+        if getattr(self, "_ranges_key", None) == key:
+            return self._ranges
+        sid = {}
+        for s, st in enumerate(stages):
+            for p in st:
+                sid[id(p)] = s
+        last = len(stages)
+        ranges = [[(0, 0)] * len(self.arenas) for _ in range(last + 1)]
+        for i, a in enumerate(self.arenas):
+            per = {}
+            for j, p in enumerate(a.params):
+                per.setdefault(sid.get(id(p), last), []).append(j)
+            for s, idx in per.items():
+                if idx[-1] - idx[0] + 1 != len(idx):
+                    raise ValueError(f"stage {s}: its parameters are not consecutive in arena {a.name!r}")
+                ranges[s][i] = (idx[0], idx[-1] + 1)
+        self._ranges_key, self._ranges = key, ranges
+        return ranges
 
     def zero_grad(self, set_to_none=False):
         for a in self.arenas:

@@ -138,6 +138,11 @@ class JEPATrainer:
                                      name="target" + a.name[7:]) for a in (enc_w, enc_n)]
         self.enc_arenas = [enc_w, enc_n]
         self.mask_tokens = list(self.pred.mask_tokens) if self.pred.mask_tokens is not None else []
+        # inputs_resident: the caller guarantees every step's clips are on the device before the
+        # previous step's update begins (bench.py: all inputs prepared up front); enables the staged
+        # update overlap (apply_update). Default off: the target forward waits for all prior work.
+        self.inputs_resident = False
+        self._staged = None
         self.reducer = None
         # time_allreduce: per step, a HIP event pair on the compute stream from the end of the backward
         # (last gradient written) to the end of GradReducer.finish() (the stream waits for every
@@ -166,9 +171,21 @@ class JEPATrainer:
         side = self._side_stream()
         if side is not None:
             main = torch.cuda.current_stream()
-            side.wait_stream(main)  # clips + this step's EMA'd target weights are ready
+            staged, self._staged = (self._staged if mask_index == 0 else None), None
+            if staged is not None:
+                # staged update (apply_update): the clips were resident before it began, so the side
+                # stream waits for that point and then for each stage's EMA'd weights as its forward
+                # reaches them, instead of for the whole optimizer pass
+                side.wait_event(staged[0])
+                for m, ev in zip(self._stage_tgt, staged[1]):
+                    m._vj_ready = ev
+            else:
+                side.wait_stream(main)  # clips + this step's EMA'd target weights are ready
             with torch.cuda.stream(side), torch.no_grad():
                 h = self.tgt.forward_features(clips, fp8=self.fp8_target, bf16_residual=self.target_bf16_residual)
+            if staged is not None:
+                for m in self._stage_tgt:
+                    m._vj_ready = None
         else:
             with torch.no_grad():
                 h = self.tgt.forward_features(clips, fp8=self.fp8_target, bf16_residual=self.target_bf16_residual)
@@ -185,6 +202,23 @@ class JEPATrainer:
                                     [B * int(m.shape[1]) for m in masks_pred], eps1=self.tgt.norm.eps, eps2=1e-5,
                                     loss_exp=self.loss_exp, npairs=npairs)
         return loss, zp, dz
+
+    def _update_stages(self):
+        """Online-encoder parameters per stage of the forward (embedding: every parameter outside the
+        blocks and the final norm; block 0 ... block L-1; final norm), and the matching target
+        modules, for the staged update."""
+        if getattr(self, "_stages", None) is None:
+            e, t = self.enc, self.tgt
+            emb = [p for n, p in e.named_parameters() if not n.startswith(("blocks.", "norm."))]
+            self._stages = [emb] + [list(b.parameters()) for b in e.blocks]
+            self._stage_tgt = [t.patch_embed] + list(t.blocks)
+            if e.norm is not None:
+                self._stages.append(list(e.norm.parameters()))
+                self._stage_tgt.append(t.norm)
+        return self._stages
+
+    def _enc_param_ids(self):
+        return {id(p) for a in self.enc_arenas for p in a.params}
 
     def _side_stream(self):
         # On by default since round 4: with the persistent one-workgroup-per-CU GEMMs and the faster
@@ -241,13 +275,25 @@ class JEPATrainer:
         """GradScaler inf-check + AdamW (train.py:446-454) + EMA (train.py:456-465). The 1/world
         average of the summed gradients is folded into AdamW. Mask tokens other than the one this
         step used have grad None in the reference, so they take no step (no decay either)."""
+        # Staged issue (inputs_resident set by the caller, target side stream on): the AdamW + EMA pass
+        # is issued stage by stage in the order the next forward uses the weights (patch embedding,
+        # block 0, ...), an event after each; the next step's target forward (side stream) waits for
+        # each stage's event instead of the whole pass, so it overlaps the rest of the update.
+        staged = (self.inputs_resident and _FUSED_EMA and self._side_stream() is not None
+                  and not any(id(t) in self._enc_param_ids() for t in self.mask_tokens))
+        pre = None
+        if staged:
+            pre = torch.cuda.Event()
+            pre.record()
         found = self.opt.check_finite() if self.mixed_precision else None
         used = {i % max(1, len(self.mask_tokens)) for i in range(getattr(self, "_groups", 1))}
         unused = [t for i, t in enumerate(self.mask_tokens) if i not in used]
         if _FUSED_EMA:  # the EMA inside the encoder arenas' AdamW pass (one read of the online weights)
             tmap = {id(o): t for t, o in zip(self.tgt_arenas, self.enc_arenas)}
-            self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused,
-                          ema=([tmap.get(id(a)) for a in self.opt.arenas], momentum))
+            evs = self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused,
+                                ema=([tmap.get(id(a)) for a in self.opt.arenas], momentum),
+                                stages=self._update_stages() if staged else None)
+            self._staged = (pre, evs) if staged else None
             self.opt.zero_grad()
         else:
             self.opt.step(grad_scale=1.0 / self.world, found_inf=found, exclude=unused)

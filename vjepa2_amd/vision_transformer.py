@@ -37,6 +37,14 @@ def sincos_3d_table(dim, grid, depth, uniform_power=False):
     return np.concatenate([_sincos_axis(dd, d), _sincos_axis(dh, h), _sincos_axis(dw, w)], axis=1)[:, :dim]
 
 
+def _wait_ready(mod):
+    """Staged optimizer update (train.JEPATrainer.apply_update): make the current stream wait for the
+    event after which this module's weights are current, when the trainer set one."""
+    ev = getattr(mod, "_vj_ready", None)
+    if ev is not None:
+        torch.cuda.current_stream().wait_event(ev)
+
+
 class PatchEmbed3D(nn.Module):
     """patch_embed.py:26-52: Conv3d with kernel = stride = (tubelet, patch, patch), run as
     im2col-of-kept-tubelets + MFMA GEMM."""
@@ -151,6 +159,7 @@ class VisionTransformer(nn.Module):
         pos = None
         if self.pos_embed is not None:
             pos = self.interpolate_pos_encoding(x, self.pos_embed)[0].float().contiguous()
+        _wait_ready(self.patch_embed)
         t = fn.run_patch_embed(x, self.patch_embed, masks, pos_table=pos, pos_ids=lay.ids, pos_mod=N)
         return t, lay
 
@@ -162,8 +171,10 @@ class VisionTransformer(nn.Module):
         if bf16_residual:
             t = ops.cast_bf16(t)
         for blk in self.blocks:
+            _wait_ready(blk)
             t = fn.run_block(t, blk, lay, fp8=fp8)
         if final_norm:
+            _wait_ready(self.norm)
             t = fn.run_layernorm(t, self.norm, out_dtype=out_dtype)
         return t, lay
 

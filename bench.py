@@ -202,7 +202,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     ms = elapsed * 1000.0 / args.steps
-    per_step = sorted(a.elapsed_time(b) for a, b in zip(marks[:-1], marks[1:]))
+    step_ms = [a.elapsed_time(b) for a, b in zip(marks[:-1], marks[1:])]  # in step order
+    per_step = sorted(step_ms)
     ms_median = per_step[len(per_step) // 2] if len(per_step) % 2 else 0.5 * (
         per_step[len(per_step) // 2 - 1] + per_step[len(per_step) // 2])
     if world > 1:
@@ -276,9 +277,14 @@ def main():
             t = torch.tensor([te], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             te = t.item()
+        # the synced steps replay the timed region's inputs (masks, hence sequence lengths) from its
+        # first step on: compare with the free-running per-step times of those same inputs
+        same = [step_ms[i % args.steps] for i in range(args.synced_steps)]
+        free_same = sum(same) / len(same)
         synced = {"ms_per_step": round(te * 1e3 / args.synced_steps, 2), "steps": args.synced_steps,
                   "sync": "float(loss) after every step (app/vjepa/train.py:468); untimed for value",
-                  "vs_free_running": round(te * 1e3 / args.synced_steps / ms, 4)}
+                  "free_running_ms_same_inputs": round(free_same, 2),
+                  "vs_free_running": round(te * 1e3 / args.synced_steps / free_same, 4)}
 
     cpu = None
     if rank == 0 and args.cpu_baseline:

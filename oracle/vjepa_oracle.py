@@ -477,18 +477,20 @@ def ac_rope_attention(x, sd, prefix, num_heads, T, H, W, action_tokens, attn_mas
     return F.linear(o, sd[prefix + "proj.weight"], sd[prefix + "proj.bias"])
 
 
-# src/models/utils/modules.py:488-497 (ACBlock with ACRoPEAttention, GELU MLP)
-def ac_block(x, sd, prefix, num_heads, T, H, W, action_tokens, attn_mask, grid_size, eps=1e-6):
+# src/models/utils/modules.py:488-497 (ACBlock with ACRoPEAttention; GELU MLP or SwiGLUFFN; draws =
+# the drop_path per-sample scales of the attention and MLP branches, or None)
+def ac_block(x, sd, prefix, num_heads, T, H, W, action_tokens, attn_mask, grid_size, eps=1e-6, draws=None):
     D = x.shape[-1]
     y = F.layer_norm(x, (D,), sd[prefix + "norm1.weight"], sd[prefix + "norm1.bias"], eps)
-    x = x + ac_rope_attention(y, sd, prefix + "attn.", num_heads, T, H, W, action_tokens, attn_mask, grid_size)
+    y = ac_rope_attention(y, sd, prefix + "attn.", num_heads, T, H, W, action_tokens, attn_mask, grid_size)
+    x = x + (y if draws is None else y * draws[0].view(-1, 1, 1))
     y = F.layer_norm(x, (D,), sd[prefix + "norm2.weight"], sd[prefix + "norm2.bias"], eps)
-    y = F.gelu(F.linear(y, sd[prefix + "mlp.fc1.weight"], sd[prefix + "mlp.fc1.bias"]))
-    return x + F.linear(y, sd[prefix + "mlp.fc2.weight"], sd[prefix + "mlp.fc2.bias"])
+    y = mlp(y, sd, prefix + "mlp.")
+    return x + (y if draws is None else y * draws[1].view(-1, 1, 1))
 
 
 # src/models/ac_predictor.py:141-190
-def ac_predictor_forward(x, actions, states, sd, cfg, extrinsics=None, eps=1e-6):
+def ac_predictor_forward(x, actions, states, sd, cfg, extrinsics=None, eps=1e-6, block_draws=None):
     gh = gw = cfg["grid"]
     x = F.linear(x, sd["predictor_embed.weight"], sd["predictor_embed.bias"])
     B, N_ctxt, D = x.shape
@@ -507,7 +509,8 @@ def ac_predictor_forward(x, actions, states, sd, cfg, extrinsics=None, eps=1e-6)
         mask = action_block_causal_mask(cfg["num_frames"] // cfg["tubelet_size"], gh, gw, cond)
         mask = mask[:x.size(1), :x.size(1)]
     for i in range(cfg["depth"]):
-        x = ac_block(x, sd, f"predictor_blocks.{i}.", cfg["num_heads"], T, gh, gw, cond, mask, gh, eps)
+        x = ac_block(x, sd, f"predictor_blocks.{i}.", cfg["num_heads"], T, gh, gw, cond, mask, gh, eps,
+                     draws=block_draws[i] if block_draws else None)
     x = x.view(B, T, cond + gh * gw, D)[:, :, cond:].flatten(1, 2)
     x = F.layer_norm(x, (D,), sd["predictor_norm.weight"], sd["predictor_norm.bias"], eps)
     return F.linear(x, sd["predictor_proj.weight"], sd["predictor_proj.bias"])

@@ -543,7 +543,10 @@ def gen_ac_predictor():
 
     out = {}
     for name, kw in (("causal", dict(use_extrinsics=False, is_frame_causal=True)),
-                     ("causal_ext", dict(use_extrinsics=True, is_frame_causal=True))):
+                     ("causal_ext", dict(use_extrinsics=True, is_frame_causal=True)),
+                     # SwiGLU MLP + stochastic depth (block 1 at rate 0.5: linspace(0, 0.5, 2)), training mode
+                     ("causal_silu_dp", dict(use_extrinsics=False, is_frame_causal=True, use_silu=True,
+                                             drop_path_rate=0.5))):
         # (is_frame_causal=False raises in the reference: ac_predictor.py:174 slices attn_mask = None)
         cfg = dict(img_size=32, patch_size=16, num_frames=6, tubelet_size=2, embed_dim=96, predictor_embed_dim=64,
                    depth=2, num_heads=2, action_embed_dim=7, **kw)
@@ -559,10 +562,12 @@ def gen_ac_predictor():
         actions = torch.randn(B, T, 7, generator=g, requires_grad=True)
         states = torch.randn(B, T, 7, generator=g, requires_grad=True)
         ext = torch.randn(B, T, 6, generator=g, requires_grad=True)
+        _DP["gen"], _DP["log"] = torch.Generator().manual_seed(38), []
         y = m(x, actions, states, ext if kw["use_extrinsics"] else None)
+        draws = list(_DP["log"])
         gy = torch.randn(y.shape, generator=g)
         y.backward(gy)
-        out[name] = dict(state={k: v.detach().clone() for k, v in m.state_dict().items()}, x=x.detach(),
+        out[name] = dict(draws=draws, state={k: v.detach().clone() for k, v in m.state_dict().items()}, x=x.detach(),
                          actions=actions.detach(), states=states.detach(), ext=ext.detach(), y=y.detach(), gy=gy,
                          gx=x.grad.detach(), gactions=actions.grad.detach(), gstates=states.grad.detach(),
                          gext=ext.grad.detach() if kw["use_extrinsics"] else None, gparams=grads_of(m), cfg=cfg,

@@ -63,13 +63,21 @@ def test_frame_causal_attention_vs_fp32(hd, H, groups, fblk):
     assert not torch.equal(o0, o)
 
 
-@pytest.mark.parametrize("which", ["causal", "causal_ext"])
+@pytest.mark.parametrize("which", ["causal", "causal_ext", "causal_silu_dp"])
 def test_ac_predictor_matches_reference(which):
+    """causal_silu_dp: SwiGLU MLPs and drop_path (block 1 at rate 0.5) in training mode, the reference's
+    per-sample draws replayed through DropPath.sample in its call order."""
     from vjepa2_amd.ac_predictor import vit_ac_predictor
 
     g = torch.load(os.path.join(GOLD, "ac_predictor.pt"), weights_only=True)[which]
     m = vit_ac_predictor(**g["cfg"]).to(DEV)
     m.load_state_dict(g["state"])
+    draws = list(g.get("draws") or [])
+    for blk in m.predictor_blocks:
+        if getattr(blk.drop_path, "drop_prob", 0):
+            mine = [draws.pop(0), draws.pop(0)]
+            blk.drop_path.sample = lambda n, device, mine=mine: mine.pop(0).to(device)
+    assert not draws
     ins = {k: g[k].to(DEV).requires_grad_(True) for k in ("x", "actions", "states", "ext")}
     y = m(ins["x"], ins["actions"], ins["states"], ins["ext"] if g["cfg"]["use_extrinsics"] else None)
     assert y.shape == g["y"].shape

@@ -176,7 +176,20 @@ def test_multiclip_golden():
         close(o, e, 1e-5, "multiclip view")
 
 
-@pytest.mark.parametrize("which", ["causal", "causal_ext"])
+def _ac_block_draws(g):
+    """The fixture's drop_path draws (flat, in the reference's call order) per predictor block: blocks
+    with rate 0 (torch.linspace(0, drop_path_rate, depth)[i] == 0) draw nothing, others attention then MLP."""
+    c = g["cfg"]
+    rates = torch.linspace(0, c.get("drop_path_rate", 0.0), c["depth"]).tolist()
+    draws = list(g.get("draws") or [])
+    out = []
+    for r in rates:
+        out.append((draws.pop(0), draws.pop(0)) if r > 0 else None)
+    assert not draws
+    return out
+
+
+@pytest.mark.parametrize("which", ["causal", "causal_ext", "causal_silu_dp"])
 def test_ac_predictor_golden(which):
     """V-JEPA 2-AC predictor (ac_predictor.py:141-190, ACRoPEAttention modules.py:163-258): the oracle
     reproduces the reference's output and every gradient (frame-causal mask, action / state /
@@ -191,7 +204,7 @@ def test_ac_predictor_golden(which):
     sd = {k: v.clone().requires_grad_(True) for k, v in g["state"].items()}
     ins = {k: g[k].clone().requires_grad_(True) for k in ("x", "actions", "states", "ext")}
     y = orc.ac_predictor_forward(ins["x"], ins["actions"], ins["states"], sd, cfg,
-                                 extrinsics=ins["ext"] if c["use_extrinsics"] else None)
+                                 extrinsics=ins["ext"] if c["use_extrinsics"] else None, block_draws=_ac_block_draws(g))
     close(y, g["y"], 1e-5, f"{which} y")
     y.backward(g["gy"])
     close(ins["x"].grad, g["gx"], 1e-5, "dx")

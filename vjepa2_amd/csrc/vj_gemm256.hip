@@ -1014,13 +1014,17 @@ int grid256(long nb, int per_cu = 1) {
 // Grouped tile order (tile rows per group): a square-ish set of the ~32 tiles an XCD has in flight
 // shares fewer A / B panels in its L2. Measured (tools/bench_kernels.py, MI355X): groups of 8 rows
 // pay on tall problems (target fc1 M = 49152: -7 %, predictor fc1 / fc2 / dgrad M = 71232: -3..-10 %)
-// and cost 2-5 % on the ~46-row-tile context problems, hence the tiles_m threshold.
+// and cost 2-5 % on the ~46-row-tile context problems (round 3). With the round-4 kernels and the
+// concurrent streams, groups of 4 rows on every problem measured best per step: +0.4 % / +0.25 % over
+// 8-or-row-major, +0.1 % over 8 on the tall ones with 4 on the rest (profiles/r04_gemm_group_ab.txt;
+// in isolation 8 is still ~1 % ahead on the target fc1 / QKV, 4 ahead on context QKV / dgrad).
 // VJ_GEMM_GROUP overrides (0 = row-major; tests: grouped order at small sizes).
 int tile_group(int tiles_m, int tiles_n) {
   const char* e = getenv("VJ_GEMM_GROUP");
   if (e) return atoi(e) > 0 ? atoi(e) : 0;
+  (void)tiles_m;
   (void)tiles_n;
-  return tiles_m >= 128 ? 8 : 0;
+  return 4;
 }
 
 template <int BN>

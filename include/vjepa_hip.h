@@ -124,6 +124,13 @@ int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const float* x, lo
                      const float* rstd, const float* gamma, const float* dres_in, long ldri, float* dres, long ldr,
                      void* dres_bf16, long ldrb, float* dgamma, float* dbeta, float* sum_in, float* sum_out, float* ws,
                      long ws_floats, void* stream);
+/* The same on the bf16 residual stream of the trained encoder under bf16 autocast (modules.py:561-562:
+ * x = x + attn(norm1(x)) is a bf16 add there): x, dres_in and dres are bf16 rows (D % 8 == 0, strides
+ * % 8, 16-B aligned), dres = bf16(dres_in + dx) with the sum in f32; column partials as above. */
+int vj_layernorm_bwd_bf16(int M, int D, const void* dy, long lddy, const void* x, long ldx, const float* mean,
+                          const float* rstd, const float* gamma, const void* dres_in, long ldri, void* dres, long ldr,
+                          float* dgamma, float* dbeta, float* sum_in, float* sum_out, float* ws, long ws_floats,
+                          void* stream);
 
 /* out[n] (+)= sum_m x[m, n]  (bias gradients), N % 8 == 0. ws >= min(256, ceil(M/64)) * N floats. */
 int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate, float* ws,

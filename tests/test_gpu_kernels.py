@@ -355,6 +355,30 @@ def test_layernorm(D, fwd, monkeypatch):
     assert torch.equal(dres2, dres) and torch.equal(dw2, dw) and torch.equal(db2, db)
     _close(s_in, 1 + dres_in.sum(0), 1e-3, 1e-4, "ln bwd sum(dres_in)")
     _close(s_out, 1 + (xr.grad + dres_in).sum(0), 1e-3, 1e-4, "ln bwd sum(dres)")
+    if D % 8:
+        return
+    # bf16 residual stream (the trained context encoder under bf16 autocast): x, dres_in bf16; dres bf16
+    # = bf16(dres_in + dLN/dx) from the f32 sum; the same column partials
+    xbr = xb.float().requires_grad_(True)
+    torch.nn.functional.layer_norm(xbr, (D,), w, b, 1e-6).backward(dy.float())
+    dres_in_b = dres_in.bfloat16()
+    exact = xbr.grad + dres_in_b.float()
+    dw3, db3 = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    s_in3, s_out3 = torch.ones(D, device=DEV), torch.ones(D, device=DEV)
+    dres3, same = ops.layernorm_bwd(dy, xb, mb, rb, w, dres_in=dres_in_b, dweight=dw3, dbias=db3, sum_in=s_in3,
+                                    sum_out=s_out3)
+    torch.cuda.synchronize()
+    assert dres3.dtype == torch.bfloat16 and same is dres3
+    # one bf16 rounding of an f32 value within 1e-4 relative of the exact sum: at most 1 ulp off
+    ulp = torch.clamp(exact.abs(), min=1e-30) * 2.0 ** -7
+    assert ((dres3.float() - exact).abs() <= ulp + 1e-5).all(), "ln bwd bf16 stream: more than 1 ulp off"
+    _close(dw3, (dy.float() * ((xb.float() - mb[:, None]) * rb[:, None])).sum(0), 1e-3, 1e-4, "ln bwd dgamma (bf16 x)")
+    _close(db3, dy.float().sum(0), 1e-3, 1e-4, "ln bwd dbeta (bf16 x)")
+    _close(s_in3, 1 + dres_in_b.float().sum(0), 1e-3, 1e-4, "ln bwd sum(dres_in) (bf16)")
+    _close(s_out3, 1 + exact.sum(0), 1e-3, 1e-4, "ln bwd sum(dres) (bf16)")
+    dres4, _ = ops.layernorm_bwd(dy, xb, mb, rb, w)  # no residual input, no column sums
+    torch.cuda.synchronize()
+    assert ((dres4.float() - xbr.grad).abs() <= torch.clamp(xbr.grad.abs(), min=1e-30) * 2.0 ** -7 + 1e-5).all()
 
 
 def test_colsum():

@@ -46,6 +46,7 @@ SIGNATURES = {
     "vj_im2col_tubelet_f32": [_I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "vj_layernorm_bwd_blocks": [_I],
     "vj_layernorm_bwd": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _L, _P, _P, _P, _P, _P, _L, _P],
+    "vj_layernorm_bwd_bf16": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P, _P, _P, _L, _P],
     "vj_colsum_f32": [_I, _I, _P, _I, _L, _P, _I, _P, _L, _P],
     "vj_rope": [_I, _I, _I, _P, _L, _I, _I, _P, _I, _I, _I, _P, _P, _I, _I, _P],
     "vj_im2col_tubelet": [_I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],

@@ -217,6 +217,11 @@ class FusedAdamW:
             if tgt is not None and not fuse:
                 late_ema.append((tgt, a))
             work.append((i, act, fuse, tgt))
+        if stages is not None and late_ema:
+            # the per-stage events would be recorded before these arenas' EMA writes, so a reader
+            # waiting on them (the next target forward) would race with it
+            raise ValueError("stages: every EMA'd arena must take the fused AdamW + EMA pass (no excluded "
+                             "parameters, equal layout)")
 
         def run(i, act, fuse, tgt, j, n):
             # maximal runs of active params with equal step count in params [j, n) of arena i

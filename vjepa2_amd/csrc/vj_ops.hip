@@ -352,13 +352,24 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int M, int D, const bf16_t* __re
 // LayerNorm backward, 16-B accesses: lane l's vector i holds the 8 columns (64 i + l) * 8 .. + 7 of
 // every operand (dy bf16 16 B, x / dres_in / dres f32 2 x 16 B, dres bf16 16 B); dres_in is loaded
 // with x and dy, before the row's reductions. Same outputs and fixed-order partials as k_ln_bwd.
-template <bool ACC, int NV, bool SUMS>
+// BFR (the bf16 residual stream of the trained encoder, the reference's autocast precision): x and
+// dres_in are bf16 rows and the result is written as bf16 only (dres_bf; dres unused): 8 B / element
+// instead of 16 + 2.
+template <bool ACC, int NV, bool SUMS, bool BFR = false>
 __global__ __launch_bounds__(256) void k_ln_bwd2(int M, int D, const bf16_t* __restrict__ dy, long lddy,
-                                                 const float* __restrict__ x, long ldx, const float* __restrict__ mean,
+                                                 const void* __restrict__ xv_, long ldx, const float* __restrict__ mean,
                                                  const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                                 const float* __restrict__ dres_in, long ldri, float* __restrict__ dres,
+                                                 const void* __restrict__ dres_in_, long ldri, float* __restrict__ dres,
                                                  long ldr, bf16_t* __restrict__ dres_bf, long ldrb, float* __restrict__ ws,
                                                  int nsum) {
+  auto unpack8 = [](const uint4& u, float (&o)[8]) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[2 * k] = __builtin_bit_cast(float, w[k] << 16);
+      o[2 * k + 1] = __builtin_bit_cast(float, w[k] & 0xffff0000u);
+    }
+  };
   constexpr int E = 8;
   __shared__ float red[4][NV * 64 * E];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -379,14 +390,25 @@ __global__ __launch_bounds__(256) void k_ln_bwd2(int M, int D, const bf16_t* __r
     for (int i = 0; i < NV; ++i) {
       if (!ok(i)) continue;
       const int c = (i * 64 + lane) * E;
-      const float4 x0 = *(const float4*)(x + row * ldx + c), x1 = *(const float4*)(x + row * ldx + c + 4);
+      float xv[E];
+      if constexpr (BFR) {
+        unpack8(*(const uint4*)((const bf16_t*)xv_ + row * ldx + c), xv);
+      } else {
+        const float* x = (const float*)xv_;
+        const float4 x0 = *(const float4*)(x + row * ldx + c), x1 = *(const float4*)(x + row * ldx + c + 4);
+        xv[0] = x0.x; xv[1] = x0.y; xv[2] = x0.z; xv[3] = x0.w; xv[4] = x1.x; xv[5] = x1.y; xv[6] = x1.z; xv[7] = x1.w;
+      }
       const uint4 u = *(const uint4*)(dy + row * lddy + c);
       if constexpr (ACC) {
-        const float4 r0 = *(const float4*)(dres_in + row * ldri + c), r1 = *(const float4*)(dres_in + row * ldri + c + 4);
-        ri[i][0] = r0.x; ri[i][1] = r0.y; ri[i][2] = r0.z; ri[i][3] = r0.w;
-        ri[i][4] = r1.x; ri[i][5] = r1.y; ri[i][6] = r1.z; ri[i][7] = r1.w;
+        if constexpr (BFR) {
+          unpack8(*(const uint4*)((const bf16_t*)dres_in_ + row * ldri + c), ri[i]);
+        } else {
+          const float* dres_in = (const float*)dres_in_;
+          const float4 r0 = *(const float4*)(dres_in + row * ldri + c), r1 = *(const float4*)(dres_in + row * ldri + c + 4);
+          ri[i][0] = r0.x; ri[i][1] = r0.y; ri[i][2] = r0.z; ri[i][3] = r0.w;
+          ri[i][4] = r1.x; ri[i][5] = r1.y; ri[i][6] = r1.z; ri[i][7] = r1.w;
+        }
       }
-      const float xv[E] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
       float gm[E];  // gamma re-read per row (cache-resident) rather than held in 16 VGPRs
       if (gamma) {
         const float4 g0 = *(const float4*)(gamma + c), g1 = *(const float4*)(gamma + c + 4);
@@ -422,9 +444,11 @@ __global__ __launch_bounds__(256) void k_ln_bwd2(int M, int D, const bf16_t* __r
         }
         if constexpr (SUMS) acc[3][i][k] += dx[k];
       }
-      *(float4*)(dres + row * ldr + c) = make_float4(dx[0], dx[1], dx[2], dx[3]);
-      *(float4*)(dres + row * ldr + c + 4) = make_float4(dx[4], dx[5], dx[6], dx[7]);
-      if (dres_bf)
+      if constexpr (!BFR) {
+        *(float4*)(dres + row * ldr + c) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+        *(float4*)(dres + row * ldr + c + 4) = make_float4(dx[4], dx[5], dx[6], dx[7]);
+      }
+      if (BFR || dres_bf)
         *(uint4*)(dres_bf + row * ldrb + c) = make_uint4(pack_bf2(dx[0], dx[1]), pack_bf2(dx[2], dx[3]),
                                                          pack_bf2(dx[4], dx[5]), pack_bf2(dx[6], dx[7]));
     }
@@ -1161,7 +1185,7 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
     const int nv8 = (D + 511) / 512;
     nbl = nb < 768 ? nb : 768;
     const int nb = nbl;
-#define LNB(AC, NVV) do { if (nsum == 4) hipLaunchKernelGGL((k_ln_bwd2<AC, NVV, true>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum); else hipLaunchKernelGGL((k_ln_bwd2<AC, NVV, false>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum); } while (0)
+#define LNB(AC, NVV) do { if (nsum == 4) hipLaunchKernelGGL((k_ln_bwd2<AC, NVV, true>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, (const void*)x, ldx, mean, rstd, gamma, (const void*)dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum); else hipLaunchKernelGGL((k_ln_bwd2<AC, NVV, false>), dim3(nb), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, (const void*)x, ldx, mean, rstd, gamma, (const void*)dres_in, ldri, dres, ldr, (bf16_t*)dres_bf16, ldrb, part, nsum); } while (0)
 #define LNB_NV(AC) switch (nv8) { case 1: LNB(AC, 1); break; case 2: LNB(AC, 2); break; case 3: LNB(AC, 3); break; default: LNB(AC, 4); }
     if (dres_in) { LNB_NV(true) }
     else { LNB_NV(false) }
@@ -1183,6 +1207,47 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
     hipLaunchKernelGGL(k_colsum2_multi, dim3((D + 31) / 32, nsum), dim3(1024), 0, st, nbl, D, ws, (long)nsum * D, o);
   }
   VJ_LAUNCH_CHECK("vj_layernorm_bwd(reduce)");
+  return VJ_OK;
+}
+
+// LayerNorm backward on the bf16 residual stream (the trained context encoder under bf16 autocast,
+// app/vjepa/train.py:437-439: x = x + attn(norm1(x)) is a bf16 add there, modules.py:561-562): x and
+// dres_in bf16 rows, dres = dres_in + dLN/dx (f32 math) written once as bf16. Same fixed-order column
+// partials (dgamma, dbeta, sums of dres_in / dres) as vj_layernorm_bwd.
+extern "C" int vj_layernorm_bwd_bf16(int M, int D, const void* dy, long lddy, const void* x, long ldx,
+                                     const float* mean, const float* rstd, const float* gamma, const void* dres_in,
+                                     long ldri, void* dres, long ldr, float* dgamma, float* dbeta, float* sum_in,
+                                     float* sum_out, float* ws, long ws_floats, void* stream) {
+  if (M == 0) return VJ_OK;
+  VJ_CHECK_ARG(D % 8 == 0 && D <= 2048, "vj_layernorm_bwd_bf16: D=%d must be %%8 and <= 2048", D);
+  VJ_CHECK_ARG(lddy % 8 == 0 && ldx % 8 == 0 && ldr % 8 == 0 && (!dres_in || ldri % 8 == 0),
+               "vj_layernorm_bwd_bf16: strides must be multiples of 8");
+  VJ_CHECK_ARG(!(((uintptr_t)dy | (uintptr_t)x | (uintptr_t)dres | (uintptr_t)dres_in) & 15),
+               "vj_layernorm_bwd_bf16: rows must be 16-B aligned");
+  VJ_CHECK_ARG(dy && x && mean && rstd && dres, "vj_layernorm_bwd_bf16: null operand");
+  VJ_CHECK_ARG(!sum_in || dres_in, "vj_layernorm_bwd_bf16: sum_in needs dres_in");
+  const int nb = vj_layernorm_bwd_blocks(M);
+  const int nsum = (sum_in || sum_out) ? 4 : ((dgamma || dbeta) ? 2 : 0);
+  if (nsum) {
+    VJ_CHECK_ARG(ws && ws_floats >= (long)nb * nsum * D, "vj_layernorm_bwd_bf16: workspace needs %ld floats",
+                 (long)nb * nsum * D);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  float* part = nsum ? ws : nullptr;
+  const int nv8 = (D + 511) / 512;
+  const int nbl = nb < 768 ? nb : 768;
+#define LNB(AC, NVV) do { if (nsum == 4) hipLaunchKernelGGL((k_ln_bwd2<AC, NVV, true, true>), dim3(nbl), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, nullptr, 0L, (bf16_t*)dres, ldr, part, nsum); else hipLaunchKernelGGL((k_ln_bwd2<AC, NVV, false, true>), dim3(nbl), dim3(256), 0, st, M, D, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, dres_in, ldri, nullptr, 0L, (bf16_t*)dres, ldr, part, nsum); } while (0)
+#define LNB_NV(AC) switch (nv8) { case 1: LNB(AC, 1); break; case 2: LNB(AC, 2); break; case 3: LNB(AC, 3); break; default: LNB(AC, 4); }
+  if (dres_in) { LNB_NV(true) }
+  else { LNB_NV(false) }
+#undef LNB_NV
+#undef LNB
+  VJ_LAUNCH_CHECK("vj_layernorm_bwd_bf16");
+  if (nsum) {
+    ColsumOuts o{{dgamma, dbeta, nsum > 2 ? sum_in : nullptr, nsum > 2 ? sum_out : nullptr}};
+    hipLaunchKernelGGL(k_colsum2_multi, dim3((D + 31) / 32, nsum), dim3(1024), 0, st, nbl, D, ws, (long)nsum * D, o);
+  }
+  VJ_LAUNCH_CHECK("vj_layernorm_bwd_bf16(reduce)");
   return VJ_OK;
 }
 

@@ -4,8 +4,10 @@ Token-major "ragged" execution: the tokens of every sequence of a pass (e.g. bot
 of a step) are concatenated into one [T, D] buffer; a TokenLayout says where the sequences are
 (attention is the only op that needs it) and which token id each row is (RoPE positions).
 
-The residual stream is kept in f32 (autocast LayerNorm semantics, train.py:438); every GEMM
-operand is bf16 with f32 accumulation. Parameter gradients are accumulated (+=) straight into
+The residual stream is f32, or bf16 where the reference's autocast keeps it in bf16 (the target
+encoder, and the trained context encoder of a RoPE model under bf16 mixed precision: the Conv3d
+output is bf16 and every x = x + branch(...) is a bf16 add; its gradient is then bf16 too); every
+GEMM operand is bf16 with f32 accumulation. Parameter gradients are accumulated (+=) straight into
 `param.grad` (f32, a view of the flat gradient arena when the trainer owns the parameters), so
 autograd only carries activation gradients between layers.
 """
@@ -247,12 +249,17 @@ def _mlp_forward(ln2, mlp, save):
 
 
 def block_forward(x, blk, lay, save):
+    """x f32, or bf16 (the residual stream in the reference's own autocast precision: the no-grad
+    target encoder, and the trained context encoder of a RoPE model under bf16 mixed precision, where
+    x = x + attn(norm1(x)) is a bf16 add, modules.py:561-562). The residual adds are fused into the
+    proj / fc2 GEMM epilogues in x's dtype."""
     T, D = x.shape
-    assert not (save and x.dtype == BF16), "the training path keeps the residual stream in f32"
     attn, mlp = blk.attn, blk.mlp
     H = attn.num_heads
     hd = D // H
     scales = _drop_scales(blk, lay, x.device)
+    if save and scales is not None and x.dtype == BF16:
+        raise NotImplementedError("drop_path on the trained bf16 residual stream (the trainer keeps f32 there)")
     ln1, m1, r1 = ops.layernorm_fwd(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, want_stats=save)
     if attn.use_rope:  # QKV GEMM with RoPE of q, k fused into its epilogue
         c, s = rope_tables(hd, x.device, lay.npos)
@@ -432,7 +439,9 @@ def block_backward(dxo, blk, lay, saved):
     T, D = x.shape
     H = attn.num_heads
     hd = D // H
-    if scales is None:
+    if dxo.dtype == BF16:  # bf16 residual stream: its gradient is bf16 too (as under the reference's autocast)
+        dy_mlp = dxo
+    elif scales is None:
         twin = getattr(dxo, "_vj_grad_bf16", None)  # bf16 twin written by the next block's LN1 backward,
         dy_mlp = twin[0] if twin is not None and twin[1] == dxo._version else ops.cast_bf16(dxo)  # unless changed
     else:  # drop_path: the MLP branch's dY = its factor x dxo (bias gradient from it, not from dxo)
@@ -465,7 +474,8 @@ def block_backward(dxo, blk, lay, saved):
     gw, gb = _ln_grads(blk.norm1)
     dxi, dxi_b = ops.layernorm_bwd(dln1, x, m1, r1, blk.norm1.weight, dres_in=dxm, dweight=gw, dbias=gb,
                                    want_bf16=True)
-    dxi._vj_grad_bf16 = (dxi_b, dxi._version)  # the previous block's fc2 dgrad / wgrad operand (saves a cast)
+    if dxi.dtype == F32:
+        dxi._vj_grad_bf16 = (dxi_b, dxi._version)  # the previous block's fc2 dgrad / wgrad operand (saves a cast)
     return dxi
 
 
@@ -597,7 +607,10 @@ def run_sublayer(x, mod, lay=None):
 # apply_masks vision_transformer.py:188-192), optional sincos pos-embed add (:183-186).
 
 
-def patch_embed_forward(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0, save=False):
+def patch_embed_forward(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0, save=False, out_bf16=False):
+    """out_bf16: the tokens in bf16 (the Conv3d's autocast output dtype, patch_embed.py:42-52), for a
+    bf16 residual stream; only without a pos-embed add (RoPE models: bf16 + an f32 table would promote
+    to f32 in the reference)."""
     proj = pe.proj
     D = proj.weight.shape[0]
     kdim = proj.weight[0].numel()
@@ -613,7 +626,8 @@ def patch_embed_forward(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0
             n = B * m.shape[1]
             ops.im2col(clip, p, tub, idx=m.contiguous(), out=cols[r0:r0 + n])
             r0 += n
-    x = ops.linear_fwd(cols, weight_bf16(proj.weight).view(D, kdim), proj.bias, EPI_F32)
+    assert not (out_bf16 and pos_table is not None), "bf16 tokens: no pos-embed add (RoPE models)"
+    x = ops.linear_fwd(cols, weight_bf16(proj.weight).view(D, kdim), proj.bias, EPI_BF16 if out_bf16 else EPI_F32)
     if pos_table is not None:
         ops.add_rows(x, pos_table, idx=pos_ids, idx_mod=pos_mod)
     return x, (cols if save else None)
@@ -621,8 +635,8 @@ def patch_embed_forward(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0
 
 class _PatchEmbedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, clip, anchor, pe, masks, pos_table, pos_ids, pos_mod):
-        x, cols = patch_embed_forward(clip, pe, masks, pos_table, pos_ids, pos_mod, save=True)
+    def forward(ctx, clip, anchor, pe, masks, pos_table, pos_ids, pos_mod, out_bf16):
+        x, cols = patch_embed_forward(clip, pe, masks, pos_table, pos_ids, pos_mod, save=True, out_bf16=out_bf16)
         ctx.pe, ctx.cols = pe, cols
         return x
 
@@ -631,17 +645,17 @@ class _PatchEmbedFn(torch.autograd.Function):
         proj = ctx.pe.proj
         D = proj.weight.shape[0]
         dx = dx.contiguous()
-        wgrad(ops.cast_bf16(dx), ctx.cols, proj.weight, (D, -1))
+        wgrad(dx if dx.dtype == BF16 else ops.cast_bf16(dx), ctx.cols, proj.weight, (D, -1))
         _bias_grad(proj, dx)
         ctx.cols = None
         _fire_hook(ctx.pe)
-        return None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None
 
 
-def run_patch_embed(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0):
+def run_patch_embed(clip, pe, masks, pos_table=None, pos_ids=None, pos_mod=0, out_bf16=False):
     if _needs_grad(None, pe):
-        return _PatchEmbedFn.apply(clip, pe.proj.weight, pe, masks, pos_table, pos_ids, pos_mod)
-    return patch_embed_forward(clip, pe, masks, pos_table, pos_ids, pos_mod)[0]
+        return _PatchEmbedFn.apply(clip, pe.proj.weight, pe, masks, pos_table, pos_ids, pos_mod, out_bf16)
+    return patch_embed_forward(clip, pe, masks, pos_table, pos_ids, pos_mod, out_bf16=out_bf16)[0]
 
 
 # ------------------------------------------------------------------------------------------------

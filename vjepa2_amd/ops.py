@@ -111,12 +111,14 @@ def wgrad_splitk(M, N, K, cus=None):
     """Split K (tokens) of a weight-gradient GEMM [M, N] += A[M, K] B[K, N]. Tiles are 256 x (256 or
     128) when M >= 256 and N >= 128 (the C side's choice), else 128 x 128. Picks the split that
     minimises (waves of tiles on the CUs) x (work per tile) + the f32 partial-slab traffic, keeping
-    >= 512 of K per slice. `cus`: the CUs the GEMM is sized for — half the chip when the weight
+    >= 512 of K per slice. `cus`: the CUs the GEMM is sized for — half the chip, since the weight
     gradients run on their own stream beside the data-gradient chain (functions.wgrad_stream: fewer
     slices, less slab traffic; +0.3 % clips/s / +0.8 % median step over 5 interleaved bench runs
-    against sizing for all 256, profiles/r04_wgrad_split_step_ab.txt), the whole chip otherwise."""
+    against sizing for all 256, profiles/r04_wgrad_split_step_ab.txt). The same sizing with the stream
+    off (VJ_WGRAD_STREAM=0): the split fixes the summation order, so the gradients are bitwise
+    independent of the stream configuration (tests/test_gpu_production.py)."""
     if cus is None:
-        cus = 128 if os.environ.get("VJ_WGRAD_STREAM", "1") == "1" else 256
+        cus = 128
     if M >= 256 and N >= 128:
         tm, tn, per_cu = 256, (256 if N % 256 == 0 else 128), 1
     else:
@@ -351,11 +353,26 @@ def layernorm_fwd(x, weight, bias, eps, out_dtype=BF16, want_stats=True):
 def layernorm_bwd(dy, x, mean, rstd, weight, dres_in=None, dweight=None, dbias=None, want_bf16=False, sum_in=None,
                   sum_out=None):
     """Returns (dres f32 = dres_in + dLN/dx, optional bf16 copy). Accumulates dweight/dbias and the
-    column sums of dres_in / dres into sum_in / sum_out (fused bias gradients)."""
+    column sums of dres_in / dres into sum_in / sum_out (fused bias gradients).
+    x bf16 (the bf16 residual stream): dres_in bf16 (or None) and dres is bf16 only -> (dres, dres)."""
     _dev(dy, x)
     M, D = x.shape
     assert dy.dtype == BF16 and dy.shape == (M, D)
     assert sum_in is None or dres_in is not None
+    if x.dtype == BF16:
+        assert dres_in is None or (dres_in.dtype == BF16 and dres_in.shape == (M, D))
+        dres = torch.empty(M, D, dtype=BF16, device=x.device)
+        nsum = 4 if (sum_in is not None or sum_out is not None) else (2 if (dweight is not None or dbias is not None) else 0)
+        ws, nws = None, 0
+        if nsum:
+            from ._lib import load
+
+            nws = load().vj_layernorm_bwd_blocks(M) * nsum * D
+            ws = torch.empty(nws, dtype=F32, device=x.device)
+        _call("vj_layernorm_bwd_bf16", M, D, _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x"), _p(mean),
+              _p(rstd), _p(weight), _p(dres_in), _rowmajor(dres_in, "dres_in") if dres_in is not None else 0, _p(dres),
+              D, _p(dweight), _p(dbias), _p(sum_in), _p(sum_out), _p(ws), nws, _stream())
+        return dres, dres
     dres = torch.empty(M, D, dtype=F32, device=x.device)
     dres_bf = torch.empty(M, D, dtype=BF16, device=x.device) if want_bf16 else None
     nsum = 4 if (sum_in is not None or sum_out is not None) else (2 if (dweight is not None or dbias is not None) else 0)

@@ -113,7 +113,7 @@ class JEPATrainer:
     """The fused V-JEPA train step (app/vjepa/train.py:409-471) over arena-owned parameters."""
 
     def __init__(self, encoder, predictor, target_encoder, optimizer, mixed_precision=True, loss_exp=1.0, world_size=1,
-                 bucket_mb=64, group=None, fp8_target=False, target_bf16_residual=None):
+                 bucket_mb=64, group=None, fp8_target=False, target_bf16_residual=None, ctx_bf16_residual=None):
         unwrap = lambda m: getattr(m, "backbone", getattr(m, "module", m))  # noqa: E731
         self.enc, self.pred, self.tgt = unwrap(encoder), unwrap(predictor), unwrap(target_encoder)
         self.opt = optimizer
@@ -129,6 +129,16 @@ class JEPATrainer:
         if target_bf16_residual is None:  # float32 configs (mixed_precision False) keep the reference's f32
             target_bf16_residual = mixed_precision and os.environ.get("VJ_TARGET_BF16", "1") != "0"
         self.target_bf16_residual = bool(target_bf16_residual)
+        # The trained context encoder's residual stream in bf16 too, where the reference's autocast keeps
+        # it there (RoPE encoder: bf16 Conv3d tokens, every x = x + branch(...) a bf16 add,
+        # modules.py:561-562; its gradient is bf16 as well). Half the bytes of its proj / fc2 residual
+        # epilogues, LayerNorm reads and LayerNorm backward. The predictor keeps f32: there
+        # torch.cat([bf16 tokens, f32 mask tokens]) promotes the stream to f32 (predictor.py:206).
+        # VJ_CTX_BF16=0 (or ctx_bf16_residual=False) keeps the context encoder's stream f32.
+        if ctx_bf16_residual is None:
+            ctx_bf16_residual = (mixed_precision and os.environ.get("VJ_CTX_BF16", "1") != "0"
+                                 and self.enc.bf16_residual_ok())
+        self.ctx_bf16_residual = bool(ctx_bf16_residual)
         enc_w, pred_w, enc_n, pred_n = optimizer.arenas
         device = enc_w.data.device
         tnamed = dict(target_encoder.named_parameters())
@@ -189,7 +199,7 @@ class JEPATrainer:
         else:
             with torch.no_grad():
                 h = self.tgt.forward_features(clips, fp8=self.fp8_target, bf16_residual=self.target_bf16_residual)
-        z, _ = self.enc.forward_ragged(clips, masks_enc, out_dtype=torch.bfloat16)
+        z, _ = self.enc.forward_ragged(clips, masks_enc, out_dtype=torch.bfloat16, bf16_residual=self.ctx_bf16_residual)
         _, Tp, Hp, Wp, _, _ = self.enc._geometry(clips)  # this group's tokens per clip (h's rows per sample)
         if h.shape[0] != B * Tp * Hp * Wp:
             raise RuntimeError(f"target rows {h.shape[0]} != {B} clips x {Tp * Hp * Wp} tokens")

@@ -145,8 +145,9 @@ class VisionTransformer(nn.Module):
                                        scale_factor=sf, mode="trilinear")
         return pe.permute(0, 2, 3, 4, 1).reshape(1, -1, dim)
 
-    def tokens(self, x, masks=None):
-        """Patch-embed the kept tubelets of every mask -> (f32 [sum_m B*K_m, D], TokenLayout)."""
+    def tokens(self, x, masks=None, out_bf16=False):
+        """Patch-embed the kept tubelets of every mask -> (f32, or bf16 with out_bf16 (RoPE models only),
+        [sum_m B*K_m, D], TokenLayout)."""
         x = x.float().contiguous()
         B, Tp, Hp, Wp, tpf, tpr = self._geometry(x)
         N = Tp * Hp * Wp
@@ -160,15 +161,28 @@ class VisionTransformer(nn.Module):
         if self.pos_embed is not None:
             pos = self.interpolate_pos_encoding(x, self.pos_embed)[0].float().contiguous()
         _wait_ready(self.patch_embed)
-        t = fn.run_patch_embed(x, self.patch_embed, masks, pos_table=pos, pos_ids=lay.ids, pos_mod=N)
+        t = fn.run_patch_embed(x, self.patch_embed, masks, pos_table=pos, pos_ids=lay.ids, pos_mod=N,
+                               out_bf16=out_bf16)
         return t, lay
+
+    def bf16_residual_ok(self):
+        """Whether the reference's bf16 autocast keeps this encoder's residual stream in bf16: the
+        Conv3d tokens are bf16 and, with RoPE, no f32 pos-embed is added (vision_transformer.py:183-186
+        would promote them to f32); and no active drop_path (not built on the bf16 training path)."""
+        return self.pos_embed is None and not any(
+            getattr(b.drop_path, "drop_prob", 0.0) and b.drop_path.training for b in self.blocks)
 
     def forward_ragged(self, x, masks, out_dtype=torch.bfloat16, final_norm=True, fp8=False, bf16_residual=False):
         """All masks in ONE pass. Returns (tokens [sum_m B*K_m, D], layout). fp8: QKV / fc1 GEMMs on
-        the fp8 MFMA (forward-only, functions.block_forward_fp8). bf16_residual (no-grad only): the
-        residual stream in bf16, as the reference's autocast keeps it (x = x + proj(...) in bf16)."""
-        t, lay = self.tokens(x, masks)
-        if bf16_residual:
+        the fp8 MFMA (forward-only, functions.block_forward_fp8). bf16_residual: the residual stream in
+        bf16, as the reference's autocast keeps it (x = x + proj(...) in bf16); with gradients (the
+        trained context encoder) only where bf16_residual_ok(), and the gradient stream is bf16 too."""
+        direct = bf16_residual and self.pos_embed is None and not fp8
+        if bf16_residual and not direct and torch.is_grad_enabled() and any(
+                p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("bf16 residual training needs a RoPE encoder without pos-embed")
+        t, lay = self.tokens(x, masks, out_bf16=direct)
+        if bf16_residual and not direct:
             t = ops.cast_bf16(t)
         for blk in self.blocks:
             _wait_ready(blk)

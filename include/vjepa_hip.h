@@ -132,6 +132,10 @@ int vj_layernorm_bwd_bf16(int M, int D, const void* dy, long lddy, const void* x
                           float* dgamma, float* dbeta, float* sum_in, float* sum_out, float* ws, long ws_floats,
                           void* stream);
 
+/* GELU(x) and GELU'(x) (nn.GELU(), vision_transformer.py:100) of n bf16 inputs, bf16 outputs, by the exact
+ * evaluation the GEMM epilogues use (the fc1 GEMM's table epilogue equals it bitwise on every bf16 input). */
+int vj_gelu_eval(int n, const void* x, void* y, void* dy, void* stream);
+
 /* out[n] (+)= sum_m x[m, n]  (bias gradients), N % 8 == 0. ws >= min(256, ceil(M/64)) * N floats. */
 int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate, float* ws,
                   long ws_floats, void* stream);

@@ -771,6 +771,42 @@ def test_gemm_staggered_matches_one_tile(K, pxcd, monkeypatch):
     assert torch.equal(res[0], res[1]), f"staggered qkv_rope != one-tile kernel (K={K} pxcd={pxcd})"
 
 
+@pytest.mark.parametrize("stg", ["1", "0"])
+def test_gelu_epilogues_bitwise_all_bf16(stg, monkeypatch):
+    """The fc1 GEMM's GELU epilogues against the exact evaluation (vj_gelu_eval: gelu_fwd_grad on the
+    bf16 input) on EVERY bf16 pre-activation: X = 0 and the bias holds the 65536 bf16 values, so
+    pre = bf16(0 + bias[n]) runs through the whole bit space. VJ_GEMM_STG=1: the staggered kernel's
+    LDS-table epilogue (GELU and GELU' looked up by the 16 input bits); 0: the one-tile kernel's direct
+    evaluation. Bitwise on every non-NaN input (the -0 pattern enters as +0: 0 + -0 = +0), NaN -> NaN."""
+    from vjepa2_amd import ops
+
+    monkeypatch.setenv("VJ_GEMM_STG", stg)
+    monkeypatch.setenv("VJ_GEMM_BM192", "0")
+    n = 65536
+    bits = torch.arange(n, dtype=torch.int32)
+    bits = torch.where(bits >= 32768, bits - 65536, bits).to(torch.int16)
+    xb = bits.view(torch.bfloat16)
+    bias = xb.float().to(DEV)
+    pre = bits.clone()
+    pre[pre == -32768] = 0  # 0 + (-0) = +0
+    y_ref, dy_ref = ops.gelu_eval(pre.view(torch.bfloat16).to(DEV).contiguous())
+    M, K = 1024, 32
+    X = torch.zeros(M, K, device=DEV, dtype=torch.bfloat16)
+    W = torch.zeros(n, K, device=DEV, dtype=torch.bfloat16)
+    d, a = ops.linear_fwd(X, W, bias, ops.EPI_GELU, out=torch.empty(M, n, device=DEV, dtype=torch.bfloat16))
+    a_ns = ops.linear_fwd(X, W, bias, ops.EPI_GELU)[1]
+    torch.cuda.synchronize()
+    nan = torch.isnan(xb.float()).to(DEV)
+    for name, got, ref in (("GELU", a, y_ref), ("GELU'", d, dy_ref), ("GELU (no save)", a_ns, y_ref)):
+        gi = got.view(torch.int16)
+        ri = ref.view(torch.int16)[None, :].expand(M, n)
+        bad = (gi != ri) & ~nan[None, :]
+        assert not bool(bad.any()), (
+            f"{name} (STG={stg}): {int(bad.sum())} mismatches, e.g. input bits "
+            f"{[hex(int(v) & 0xffff) for v in bits[bad[0].cpu()][:8]]}")
+        assert bool(torch.isnan(got.float()[:, nan]).all()), f"{name}: NaN input must give NaN"
+
+
 @pytest.mark.parametrize("K", [64, 128, 1024])
 @pytest.mark.parametrize("pxcd", [None, "1"])
 def test_gemm_192_row_tiles_match_256(K, pxcd, monkeypatch):

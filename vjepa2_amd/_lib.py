@@ -46,6 +46,7 @@ SIGNATURES = {
     "vj_im2col_tubelet_f32": [_I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P],
     "vj_layernorm_bwd_blocks": [_I],
     "vj_layernorm_bwd": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _L, _P, _P, _P, _P, _P, _L, _P],
+    "vj_gelu_eval": [_I, _P, _P, _P, _P],
     "vj_layernorm_bwd_bf16": [_I, _I, _P, _L, _P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _P, _P, _P, _P, _L, _P],
     "vj_colsum_f32": [_I, _I, _P, _I, _L, _P, _I, _P, _L, _P],
     "vj_rope": [_I, _I, _I, _P, _L, _I, _I, _P, _I, _I, _I, _P, _P, _I, _I, _P],
@@ -87,7 +88,11 @@ def load():
         )
     lib = ctypes.CDLL(LIB_PATH)
     for name, args in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if os.environ.get("VJ_LIB"):  # an older build selected for an A/B run: its own symbol set
+                continue
+            raise RuntimeError(f"{LIB_PATH} does not export {name}: stale build (rebuild the extension)")
         fn.argtypes = args
         fn.restype = ctypes.c_int
     _lib = lib

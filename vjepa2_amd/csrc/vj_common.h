@@ -52,8 +52,11 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32 on gfx950
   return __builtin_bit_cast(bf16_t, b);
 }
+// Two values -> one packed bf16 pair with ONE v_cvt_pk_bf16_f32 (the same RNE conversion as f2bf; the
+// scalar form compiled to two conversions + a shift + an or_sdwa per pair)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2_t));
 }
 
 // ----- cross-lane exchanges on the VALU (DPP / gfx950 permlane swaps) -----
@@ -167,7 +170,10 @@ static inline int vj_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 // The argument is pre-scaled by sqrt(log2 e) (zs = z sqrt(log2 e), the A-S constant divided by the
 // same) so the Gaussian is one v_exp_f32 (exp2) of -zs^2 with no extra multiply, and the CDF is one
 // fma: 14 -> 12 VALU per element besides the two transcendentals.
-__device__ __forceinline__ void gelu_fwd_grad(float x, float& y, float& dy) {
+// gelu_cdf_grad gives the multiplier cdf = Phi(x) (GELU(x) = x * cdf, exactly as below) and GELU'(x);
+// the GEMM's table epilogue (vj_gemm_tile.h) stores these two per bf16 input, so its y = x * cdf is the
+// same f32 operation on the same operands as here.
+__device__ __forceinline__ void gelu_cdf_grad(float x, float& cdf, float& dy) {
   const float zs = x * 0.84932180028801904f;  // x / sqrt(2) * sqrt(log2 e)
   const float a = fabsf(zs);
   const float t = __builtin_amdgcn_rcpf(fmaf(0.27273748087922250f, a, 1.f));  // 0.3275911 / sqrt(log2 e)
@@ -177,9 +183,13 @@ __device__ __forceinline__ void gelu_fwd_grad(float x, float& y, float& dy) {
   p = fmaf(p, t, 0.254829592f);
   p *= t;
   const float e = __builtin_amdgcn_exp2f(-zs * zs);  // exp(-x^2 / 2)
-  const float cdf = fmaf(0.5f, copysignf(fmaf(-p, e, 1.f), zs), 0.5f);
-  y = x * cdf;
+  cdf = fmaf(0.5f, copysignf(fmaf(-p, e, 1.f), zs), 0.5f);
   dy = fmaf(x * 0.39894228040143268f, e, cdf);
+}
+__device__ __forceinline__ void gelu_fwd_grad(float x, float& y, float& dy) {
+  float cdf;
+  gelu_cdf_grad(x, cdf, dy);
+  y = x * cdf;
 }
 
 // 3-axis RoPE applied to the q and k columns of a fused QKV projection (modules.py:26-50, 343-365),

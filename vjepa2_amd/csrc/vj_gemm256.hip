@@ -92,11 +92,16 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   constexpr bool EARLY1 = DIRECT && !AUX;
   // STG: ring of NSL 32-KB unit slots, DMA distance NSL - 2 units; 5 slots (all 160 KB of the CU's
   // LDS, distance 3) unless the RoPE epilogue needs the table area (4 slots + table, distance 2)
-  constexpr int NSL = STG ? (EPI == EPI_ROPE ? 4 : 5) : 1;
+  // (GTAB: the GELU epilogue by table, 4 slots behind the 28.7-KB table at LDS offset 0, whose byte
+  // offsets then fit the 16-bit lanes the lookup computes them in)
+  constexpr bool GTAB = STG && EPI == EPI_GELU;
+  constexpr int NSL = STG ? ((EPI == EPI_ROPE || GTAB) ? 4 : 5) : 1;
   constexpr int DIST = NSL - 2;
-  __shared__ __attribute__((aligned(16))) char smem_raw[STG && NSL == 5 ? 5 * 32768 : 2 * STAGE + TAB_BYTES];
+  constexpr int RING0 = GTAB ? 32768 : 0;  // LDS offset of the STG ring
+  __shared__ __attribute__((aligned(16))) char smem_raw[GTAB ? RING0 + 4 * 32768 : STG && NSL == 5 ? 5 * 32768 : 2 * STAGE + TAB_BYTES];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   LDS_AS char* tab = smem + 2 * STAGE;
+  [[maybe_unused]] LDS_AS char* ring = smem + RING0;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // this wave's pieces 2h, 2h + 1 of stream position dpos (into slot dpos % NSL)
   auto dma_half = [&](auto h_c) {
     constexpr int h = decltype(h_c)::value;
-    LDS_AS char* dst = smem + (dpos % NSL) * USZ + (isA ? 0 : 16384) + (4 * (wave & 3) + 2 * h) * 1024;
+    LDS_AS char* dst = ring + (dpos % NSL) * USZ + (isA ? 0 : 16384) + (4 * (wave & 3) + 2 * h) * 1024;
     const int soff = __builtin_amdgcn_readfirstlane(dku * 64);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst, 16, dvo[2 * h], soff, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst + 1024, 16, dvo[2 * h + 1], soff, 0, 0);
@@ -261,6 +266,9 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       if (e < ntab) rtab[e] = rpf[i];
     }
   }
+  // GELU table: computed once per (persistent) workgroup under the first units' DMA; read only in the
+  // epilogues, after the first tile's barriers
+  if constexpr (GTAB) gelu_tab_fill((LDS_AS f32x2*)smem, threadIdx.x, NT);
 
   // Accumulators: acc[i][j] = m-tile i (16 rows), n block j; the epilogue walks the 2 * MH m-tiles,
   // 4 rows per lane (rows rowoff(i) + 4 (lane >> 4) + r of the wave tile).
@@ -441,7 +449,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         __builtin_amdgcn_sched_barrier(0);
       };
       for (int u = 0; u < nku; ++u) {
-        const LDS_AS char* sA = smem + ((q0 + u) % NSL) * USZ;
+        const LDS_AS char* sA = ring + ((q0 + u) % NSL) * USZ;
         const LDS_AS char* sB = sA + 16384;
 #pragma unroll
         for (int i = 0; i < 4; ++i) Aa[i] = frag<true, 256, 32>(sA, wr * 128 + i * 16, 0, lane);
@@ -831,8 +839,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
                                      v[2 * q2 + 1] * aux[i % (AUX_PF + 1)][r][2 * q2 + 1]);
               else
                 pk[r][q2] = pack_bf2(v[2 * q2], v[2 * q2 + 1]);
-              if constexpr (EPI == EPI_GELU)  // pk: the bf16 pre-activation -> GELU, derivative (if saved)
-                ga[r][q2] = gelu_pair(pk[r][q2], SAVE_D ? &pk[r][q2] : nullptr);
+              if constexpr (EPI == EPI_GELU) {  // pk: the bf16 pre-activation -> GELU, derivative (if saved)
+                if constexpr (GTAB) ga[r][q2] = gelu_pair_tab<SAVE_D>(pk[r][q2], smem, &pk[r][q2]);
+                else ga[r][q2] = gelu_pair(pk[r][q2], SAVE_D ? &pk[r][q2] : nullptr);
+              }
             }
           }
         }

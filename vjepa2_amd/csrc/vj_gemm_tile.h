@@ -128,6 +128,58 @@ __device__ __forceinline__ uint32_t gelu_pair(uint32_t pk, uint32_t* dpk) {
   return pack_bf2(y0, y1);
 }
 
+// ---- GELU by table (the staggered fc1 kernel's epilogue). The pre-activation is a bf16 value (the
+// reference's autocast rounding point), so GELU(pre) and GELU'(pre) are functions of its 16 bits.
+// Entry (i, s) of the LDS table (interleaved: byte 16 i + 8 s) holds {cdf, dy} = gelu_cdf_grad(x) for
+// x = (-1)^s * bf16(GT_LO - 1 + i) (i >= 1), x = (-1)^s * 0 (i = 0); the epilogue forms y = x * cdf,
+// the same f32 product gelu_fwd_grad takes, and dy as stored. Magnitudes outside [2^-10, 16) share
+// one entry per side because their bf16 outputs are the same:
+//  * |x| < 2^-10 -> the +-0 entry: cdf(x) = 0.5 +- 0.4|x| stays within 2^-10.3 of 0.5 (relative),
+//    inside half a bf16 ulp of x / 2 for y and of 0.5 for dy; below 2^-24 cdf(x) IS cdf(+-0) (rcp(1 +
+//    0.27 a) = 1, exp2(-zs^2) = 1), which keeps the f32-denormal products (round-half-even ties of
+//    x / 2 in bf16) those of the exact evaluation;
+//  * |x| >= 16 -> the largest entry below 16: exp2(-zs^2) underflows to 0, so cdf = 1 (x > 0) or
+//    0 (x < 0) and dy = 1 or 0 exactly, as for every larger |x|;
+//  * inf / NaN: y = x * cdf gives what the exact evaluation gives; dy = fma(x, 0, dy_tab) is NaN for
+//    them (x * 0) and dy_tab otherwise (dy is never -0).
+// ~9 VALU + one LDS read per element instead of ~17 VALU + rcp + exp2; bitwise equal to gelu_fwd_grad
+// on all 65536 bf16 inputs (tests/test_gpu_kernels.py::test_gelu_epilogues_bitwise_all_bf16).
+constexpr uint32_t GT_LO = 0x3A80;       // bf16 bits of 2^-10
+constexpr uint32_t GT_HI = 0x417F;       // largest bf16 below 16
+constexpr int GT_N = GT_HI - GT_LO + 2;  // entries per sign (index 0: |x| < 2^-10, zero, denormals)
+constexpr int GT_BYTES = 2 * GT_N * 8;   // 28.7 KB
+
+__device__ __forceinline__ void gelu_tab_fill(LDS_AS f32x2* tab, int tid, int nthreads) {
+  for (int e = tid; e < 2 * GT_N; e += nthreads) {
+    const uint32_t i = (uint32_t)e >> 1, sg = (uint32_t)e & 1;
+    const uint32_t bits = (i == 0 ? 0u : GT_LO - 1 + i) | (sg << 15);
+    float cdf, dy;
+    gelu_cdf_grad(__builtin_bit_cast(float, bits << 16), cdf, dy);
+    tab[e] = f32x2{cdf, dy};
+  }
+}
+
+// GELU (and GELU' into *dpk when SAVE_D) of the two bf16 pre-activations packed in pk, by table
+template <bool SAVE_D>
+__device__ __forceinline__ uint32_t gelu_pair_tab(uint32_t pk, const LDS_AS char* tab, uint32_t* dpk) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 b = __builtin_bit_cast(u16x2, pk);
+  u16x2 i = __builtin_elementwise_sub_sat(b & (u16x2)0x7fff, (u16x2)(GT_LO - 1));
+  i = __builtin_elementwise_min(i, (u16x2)(GT_N - 1));
+  const uint32_t a = __builtin_bit_cast(uint32_t, (u16x2)((i << 4) | ((b >> 12) & (u16x2)8)));
+  const float x0 = __builtin_bit_cast(float, pk << 16), x1 = __builtin_bit_cast(float, pk & 0xffff0000u);
+  if constexpr (SAVE_D) {
+    const f32x2 t0 = *(const LDS_AS f32x2*)(tab + (a & 0xffffu));
+    const f32x2 t1 = *(const LDS_AS f32x2*)(tab + (a >> 16));
+    *dpk = pack_bf2(fmaf(x0, 0.f, t0[1]), fmaf(x1, 0.f, t1[1]));
+    return pack_bf2(x0 * t0[0], x1 * t1[0]);
+  } else {
+    const float c0 = *(const LDS_AS float*)(tab + (a & 0xffffu));
+    const float c1 = *(const LDS_AS float*)(tab + (a >> 16));
+    return pack_bf2(x0 * c0, x1 * c1);
+  }
+}
+
 struct Tile {
   int m0, n0, z, Keff, nk;  // buffer descriptors are rebuilt per DMA: SGPRs are the scarce resource
 };

@@ -1210,6 +1210,29 @@ extern "C" int vj_layernorm_bwd(int M, int D, const void* dy, long lddy, const f
   return VJ_OK;
 }
 
+// GELU and GELU' of bf16 inputs by the GEMM epilogues' exact evaluation (gelu_fwd_grad): the reference
+// the table epilogue of the fc1 GEMM is checked against, bitwise, over every bf16 input.
+namespace {
+__global__ __launch_bounds__(256) void k_gelu_eval(int n, const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                   bf16_t* __restrict__ dy) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float a, d;
+  gelu_fwd_grad(bf2f(x[i]), a, d);
+  y[i] = f2bf(a);
+  dy[i] = f2bf(d);
+}
+}  // namespace
+
+extern "C" int vj_gelu_eval(int n, const void* x, void* y, void* dy, void* stream) {
+  if (n == 0) return VJ_OK;
+  VJ_CHECK_ARG(n > 0 && x && y && dy, "vj_gelu_eval: bad arguments");
+  hipLaunchKernelGGL(k_gelu_eval, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, (const bf16_t*)x,
+                     (bf16_t*)y, (bf16_t*)dy);
+  VJ_LAUNCH_CHECK("vj_gelu_eval");
+  return VJ_OK;
+}
+
 // LayerNorm backward on the bf16 residual stream (the trained context encoder under bf16 autocast,
 // app/vjepa/train.py:437-439: x = x + attn(norm1(x)) is a bf16 add there, modules.py:561-562): x and
 // dres_in bf16 rows, dres = dres_in + dLN/dx (f32 math) written once as bf16. Same fixed-order column

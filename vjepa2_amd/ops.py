@@ -662,6 +662,15 @@ def ema(target, online, momentum, target_bf16=None):
     _call("vj_ema", target.numel(), _p(target), _p(online), float(momentum), _p(target_bf16), _stream())
 
 
+def gelu_eval(x):
+    """(GELU(x), GELU'(x)) bf16 of bf16 x by the GEMM epilogues' exact evaluation (vj_gelu_eval)."""
+    _dev(x)
+    assert x.dtype == BF16 and x.is_contiguous()
+    y, dy = torch.empty_like(x), torch.empty_like(x)
+    _call("vj_gelu_eval", x.numel(), _p(x), _p(y), _p(dy), _stream())
+    return y, dy
+
+
 def cast_bf16(x, out=None):
     _dev(x)
     assert x.dtype == F32 and x.is_contiguous()

@@ -92,6 +92,9 @@ def main():
     ap.add_argument("--fp8-target", type=int, default=0, help="target encoder QKV / fc1 GEMMs on the fp8 MFMA")
     ap.add_argument("--synced-steps", type=int, default=5,
                     help="untimed comparison steps with a float(loss) host sync per step (0: skip)")
+    ap.add_argument("--arm-reducer", type=int, default=0,
+                    help="at --gpus 1: arm the bucketed gradient all-reduce over a one-rank process group "
+                         "(VJ_DIST_BACKEND, default nccl = RCCL) to price what N > 1 adds to the step")
     args = ap.parse_args()
     if args.gpus > 1 and "RANK" not in os.environ:
         # no launcher: start one rank process per GPU from this GPU-free parent
@@ -111,8 +114,18 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} rank(s)")
     dev = torch.device("cuda", local_rank)
+    if args.arm_reducer and world == 1 and not dist.is_initialized():
+        import socket
+
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        backend = os.environ.get("VJ_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                **({"device_id": dev} if backend == "nccl" else {}))
     # every rank states its process group (RCCL carried the buckets iff backend == "nccl")
-    print(f"[bench rank {rank}/{world}] backend={dist.get_backend() if world > 1 else None} device={dev}",
+    print(f"[bench rank {rank}/{world}] backend={dist.get_backend() if dist.is_initialized() else None} device={dev}",
           file=sys.stderr, flush=True)
     B, T, S = args.batch, args.frames, args.crop
     N = (T // 2) * (S // 16) ** 2
@@ -128,8 +141,9 @@ def main():
     opt, scaler, sched, wds = init_opt(enc, pred, iterations_per_epoch=300, start_lr=1e-4, ref_lr=5.25e-4, warmup=40,
                                        num_epochs=10, wd=0.04, final_wd=0.04, final_lr=5.25e-4, ipe_scale=1.25,
                                        mixed_precision=True)
+    armed = args.arm_reducer == 1 or world > 1  # --arm-reducer 2: the process group only (diagnostics)
     trainer = JEPATrainer(enc, pred, tgt, opt, mixed_precision=True, loss_exp=1.0, world_size=world,
-                          fp8_target=bool(args.fp8_target))
+                          fp8_target=bool(args.fp8_target), arm_reducer=armed)
     # every step's clips and masks are on the device before the first step (below): the next step's
     # target forward may start under the previous step's staged update (JEPATrainer.apply_update)
     trainer.inputs_resident = os.environ.get("VJ_STAGED_UPDATE", "1") == "1"
@@ -302,7 +316,8 @@ def main():
                "value_is": "whole-job clips/s (all ranks' clips / max-over-ranks time); per GPU: clips_per_s_per_gpu",
                "clips_per_s_per_gpu": round(value / world, 3), "ms_per_step_median": round(ms_median, 2),
                "clips_per_s_per_gpu_median": round(B / (ms_median * 1e-3), 3),
-               "dist_backend": dist.get_backend() if world > 1 else None, "step_tflop": round(flops / 1e12, 2),
+               "dist_backend": dist.get_backend() if dist.is_initialized() else None,
+               "reducer_armed": armed, "step_tflop": round(flops / 1e12, 2),
                "step_tflops_per_gpu": round(flops / (ms * 1e-3) / 1e12, 1),
                "mfu_bf16": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                "loss_last": round(float(loss.item()), 5), "allreduce_exposed_ms": round(ar_ms, 3),
@@ -312,7 +327,7 @@ def main():
                                   "tflops": round(v["flops"] / (v["total_ms"] * 1e-3) / 1e12, 1) if v["flops"] else None}
                               for k, v in sorted(kstats.items(), key=lambda kv: -kv[1]["total_ms"])}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

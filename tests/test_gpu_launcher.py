@@ -101,3 +101,16 @@ def test_bench_gpus2_spawns_two_ranks():
     for rk in (0, 1):
         assert f"[bench rank {rk}/2] backend=gloo" in r.stderr, r.stderr[-2000:]
     print(lines[0][:400])
+
+
+def test_bench_one_gpu_armed_reducer_over_rccl():
+    """`bench.py --arm-reducer 1` at one GPU: the bucketed gradient all-reduce armed over a one-rank
+    RCCL ("nccl") process group, the collective path of a DP run on one device."""
+    r = _run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--batch", "2", "--crop", "64", "--frames",
+              "8", "--model", "vit_small", "--cpu-baseline", "0", "--kernel-events", "0", "--arm-reducer", "1"],
+             _env(), timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["reducer_armed"] is True and out["dist_backend"] == "nccl"
+    assert out["allreduce_exposed_ms"] > 0 and 0.0 < out["loss_last"] < 10.0
+    assert "[bench rank 0/1] backend=nccl" in r.stderr, r.stderr[-2000:]

@@ -95,19 +95,35 @@ class GradReducer:
             b.work = None
         self.next = 0
 
+    def _all_reduce(self, b):
+        b.work = dist.all_reduce(b.view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
     def _issue(self, b):
         # With the weight-gradient stream on (functions.wgrad_stream), the bucket's weight gradients
-        # may still be in flight there: issue from that stream after it has waited for the current
-        # one (the LayerNorm / bias gradients written there), so the collective sees both.
-        from .functions import wgrad_stream
+        # may still be in flight there, and its LayerNorm / bias gradients were written on the current
+        # stream. The collective is queued to go out on the weight-gradient stream right after that
+        # stream's next join with the current one (the next block's first weight-gradient launch, a few
+        # launches later), so it sees both without a join of its own: a join per bucket cost 2.8 % of
+        # the step (profiles/r05_reducer_joins_ab.txt). Queue order = bucket order on every rank.
+        from . import functions
 
-        side = wgrad_stream()
+        side = functions.wgrad_stream()
         if side is None:
-            b.work = dist.all_reduce(b.view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self._all_reduce(b)
             return
+        functions._AFTER_JOIN.append(lambda b=b: self._all_reduce(b))
+
+    def _flush(self):
+        """Issue the queued collectives now: one join of the weight-gradient stream with the current."""
+        from . import functions
+
+        if not functions._AFTER_JOIN:
+            return
+        side = functions.wgrad_stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            b.work = dist.all_reduce(b.view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            while functions._AFTER_JOIN:
+                functions._AFTER_JOIN.pop(0)()
 
     def mark_ready(self, module):
         """Hook called when `module`'s backward has finished writing its parameter gradients."""
@@ -132,6 +148,7 @@ class GradReducer:
             self.next += 1
         for b in self.tail:
             self._issue(b)
+        self._flush()
         for b in self.buckets + self.tail:
             b.work.wait()
         self.reset()

@@ -346,6 +346,11 @@ def join_wgrad_stream():
 
 
 _WG_JOIN_TASK = [None]  # autograd graph task whose end-of-backward join is queued
+# Work to issue on the weight-gradient stream right after its next join with the current stream
+# (distributed.GradReducer: a bucket's all-reduce also needs the LayerNorm / bias gradients written on
+# the current stream; riding on the join every block's weight gradients take anyway saves a join of
+# its own per bucket).
+_AFTER_JOIN = []
 
 
 def _join_at_backward_end():
@@ -376,6 +381,8 @@ class _OnWgradStream:
             _WG_JOIN_TASK[0] = task
         self.ctx = torch.cuda.stream(self.side)
         self.ctx.__enter__()
+        while _AFTER_JOIN:
+            _AFTER_JOIN.pop(0)()
         return self
 
     def __exit__(self, *exc):

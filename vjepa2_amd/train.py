@@ -113,7 +113,8 @@ class JEPATrainer:
     """The fused V-JEPA train step (app/vjepa/train.py:409-471) over arena-owned parameters."""
 
     def __init__(self, encoder, predictor, target_encoder, optimizer, mixed_precision=True, loss_exp=1.0, world_size=1,
-                 bucket_mb=64, group=None, fp8_target=False, target_bf16_residual=None, ctx_bf16_residual=None):
+                 bucket_mb=64, group=None, fp8_target=False, target_bf16_residual=None, ctx_bf16_residual=None,
+                 arm_reducer=False):
         unwrap = lambda m: getattr(m, "backbone", getattr(m, "module", m))  # noqa: E731
         self.enc, self.pred, self.tgt = unwrap(encoder), unwrap(predictor), unwrap(target_encoder)
         self.opt = optimizer
@@ -159,7 +160,9 @@ class JEPATrainer:
         # bucket): the all-reduce time NOT hidden under the backward. Appended to ar_events.
         self.time_allreduce = False
         self.ar_events = []
-        if world_size > 1:
+        # arm_reducer: the gradient all-reduce even at world 1 (a one-rank process group): prices what the
+        # bucketed all-reduce and its stream joins add to the step on one GPU (bench.py --arm-reducer)
+        if world_size > 1 or arm_reducer:
             seg = lambda a: (a.grad, [(p, o, p.numel()) for p, o in zip(a.params, a.offsets)])  # noqa: E731
             self.reducer = GradReducer([seg(pred_w), seg(enc_w)], tail_segments=[seg(pred_n), seg(enc_n)],
                                        bucket_mb=bucket_mb, group=group)

@@ -218,7 +218,12 @@ def _drop_scales(blk, lay, device):
     dp = blk.drop_path
     if not getattr(dp, "drop_prob", None) or not dp.training:
         return None
-    lens = torch.tensor([ln for n, ln in lay.groups for _ in range(n)], device=device)
+    lens = getattr(lay, "_vj_seq_lens", None)  # built once per layout (one H2D copy, not one per block)
+    if lens is None or lens.device != torch.device(device):
+        lens = lay._vj_seq_lens = torch.tensor([ln for n, ln in lay.groups for _ in range(n)], device=device)
+    # One draw per sequence for all packed mask groups at once (the reference's MultiSeqWrapper runs one
+    # forward per mask and draws per mask): the same distribution, another RNG stream order, so a
+    # multi-mask drop_path run is not replayable from the reference's seed (single-group fixtures are).
     return tuple(dp.sample(lens.numel(), device).repeat_interleave(lens, output_size=lay.T) for _ in range(2))
 
 

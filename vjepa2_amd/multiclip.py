@@ -5,6 +5,8 @@ concatenated along time, and an optional 1-D temporal sincos embedding is added 
 indices. The encoder is the HIP VisionTransformer; the optional embedding add is vj_add_rows.
 """
 
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -60,9 +62,10 @@ class ClipAggregation(nn.Module):
                 # row (b, c, t, s) += pos_embed[clip_indices[c][b, t * tubelet]] (apply_masks of the table)
                 idx = torch.stack([ci[:, ::self.tubelet_size] for ci in clip_indices], 1)  # [B, clips, T]
                 # CPU indices (the eval loaders' clip_indices) are validated here and raise as the
-                # reference's gather would; device indices are not read back (no host sync per forward):
-                # vj_add_rows never reads a table row outside [0, rows) and leaves such a row unchanged
-                if not idx.is_cuda:
+                # reference's gather would; device indices are not read back (no host sync per forward)
+                # unless VJ_CHECK_INDICES=1 (debug): vj_add_rows never reads a table row outside
+                # [0, rows) and leaves such a row unchanged
+                if not idx.is_cuda or os.environ.get("VJ_CHECK_INDICES", "0") == "1":
                     lo, hi = int(idx.min()), int(idx.max())
                     if lo < 0 or hi >= self.pos_embed.shape[1]:
                         raise IndexError(f"clip index {hi if hi >= self.pos_embed.shape[1] else lo} out of range "

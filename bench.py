@@ -27,6 +27,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "clips/sec/GPU (ViT-L/16, 16×256², bf16) fwd+bwd; 1→8 GPU scaling"
+MODEL_LABELS = {"vit_large": "ViT-L", "vit_small": "ViT-S", "vit_huge": "ViT-H", "vit_giant": "ViT-g",
+                "vit_giant_xformers": "ViT-g"}
+
+
+def metric_for(model, frames, crop, fp8=False):
+    """BASELINE's metric string, naming the model / clip shape / precision the line actually ran
+    (BASELINE.json's own string for its ViT-L/16 16x256^2 bf16 config)."""
+    if (model, frames, crop, fp8) == ("vit_large", 16, 256, False):
+        return METRIC
+    dt = "bf16, fp8 target QKV/fc1" if fp8 else "bf16"
+    return f"clips/sec/GPU ({MODEL_LABELS.get(model, model)}/16, {frames}×{crop}², {dt}) fwd+bwd; 1→8 GPU scaling"
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP8_TFLOPS = 5000.0  # dense fp8 (block-scaled e4m3 MFMA: 2x bf16 per clock)
 PEAK_HBM_GBS = 8000.0
@@ -305,7 +316,7 @@ def main():
         cpu = cpu_baseline(args, data[0])
 
     if rank == 0:
-        out = {"metric": METRIC, "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
+        out = {"metric": metric_for(args.model, T, S, bool(args.fp8_target)), "value": round(value, 3), "unit": "clips/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": round(ms, 2), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "bf16+fp8(target QKV/fc1)" if args.fp8_target else "bf16",
                "data": "synthetic",

@@ -13,6 +13,10 @@ timeout -k 10 300 python -u bench.py > "$out/bench.log" 2>&1 || { echo "bench fa
 tail -c 600 "$out/bench.log"
 VJ_TGT_STREAM=0 VJ_WGRAD_STREAM=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --kernel-events 0 --synced-steps 0 > "$out/prof.log" 2>&1 || { echo "prof failed"; tail -5 "$out/prof.log"; exit 4; }
 echo "prof ok"
+# per-step kernel table from the trace's steady-state window (tools/prof_summary.py: setup excluded)
+python3 tools/prof_summary.py "$(find "$out/prof" -name '*kernel_trace.csv' | head -1)" 4 "$out/kernel_stats.txt" \
+  "VJ_TGT_STREAM=0 VJ_WGRAD_STREAM=0 python3 bench.py --steps 3 --warmup 1 --cpu-baseline 0 --kernel-events 0 --synced-steps 0 (serialised)" \
+  || { echo "prof summary failed"; exit 4; }
 bash tools/pmc_bench.sh "$tag" > "$out/pmc.log" 2>&1 || { echo "pmc failed"; tail -5 "$out/pmc.log"; exit 5; }
 echo "pmc ok"
 # the bench's own dominant kernel (roofline.kernel of its JSON line)

@@ -111,14 +111,15 @@ def wgrad_splitk(M, N, K, cus=None):
     """Split K (tokens) of a weight-gradient GEMM [M, N] += A[M, K] B[K, N]. Tiles are 256 x (256 or
     128) when M >= 256 and N >= 128 (the C side's choice), else 128 x 128. Picks the split that
     minimises (waves of tiles on the CUs) x (work per tile) + the f32 partial-slab traffic, keeping
-    >= 512 of K per slice. `cus`: the CUs the GEMM is sized for — half the chip, since the weight
-    gradients run on their own stream beside the data-gradient chain (functions.wgrad_stream: fewer
-    slices, less slab traffic; +0.3 % clips/s / +0.8 % median step over 5 interleaved bench runs
-    against sizing for all 256, profiles/r04_wgrad_split_step_ab.txt). The same sizing with the stream
-    off (VJ_WGRAD_STREAM=0): the split fixes the summation order, so the gradients are bitwise
-    independent of the stream configuration (tests/test_gpu_production.py)."""
+    >= 512 of K per slice. `cus`: the CUs the GEMM is sized for — the whole chip. With the weight
+    gradients on their own stream (functions.wgrad_stream) sizing for half the chip measured the same
+    step time (round 5: 222.6 vs 222.7 clips/s; round 4 had read +0.3 % for it, inside the noise),
+    for 64 / 32 CUs 5 / 8 % slower (profiles/r05_wgrad_experiments_step_ab.txt); run alone (the
+    serialised profile) the half-chip split left half the CUs idle. The split does not depend on the
+    stream setting: it fixes the summation order, so the gradients are bitwise independent of the
+    stream configuration (tests/test_gpu_production.py)."""
     if cus is None:
-        cus = 128
+        cus = 256
     if M >= 256 and N >= 128:
         tm, tn, per_cu = 256, (256 if N % 256 == 0 else 128), 1
     else:

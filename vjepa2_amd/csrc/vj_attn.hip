@@ -288,6 +288,46 @@ __device__ __forceinline__ bf16x8 gload8(const bf16_t* p, bool ok) {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// A wave's 32 x HD output tile (O, dQ, dK or dV) held as accumulators x[d] (token = lane & 31, head
+// dim d*32 + acc_row(r, lane)), stored through LDS as whole rows: the lane's 4 consecutive dims
+// (accumulator rows 4j..4j+3) go to a wave-private LDS image (16-B chunks XOR-swizzled by row), read
+// back as 16-B row chunks and stored 64 / (HD/8) rows per instruction. Replaces 4-B stores at a row
+// stride, where every store instruction touched 32-64 cache lines.
+template <int HD>
+struct OutTile {
+  static constexpr int NCH = HD / 8;  // 16-B chunks stored per row
+  static constexpr int CH = Hd<HD>::P / 8 <= 4 ? 4 : (Hd<HD>::P / 8 <= 8 ? 8 : 16);  // per LDS row
+  static constexpr int SWM = CH < 8 ? CH - 1 : 7;
+  static constexpr int BYTES = 32 * CH * 16;  // one wave's image
+};
+template <int HD>
+__device__ __forceinline__ void wave_store_rows(const f32x16 (&x)[Hd<HD>::P / 32], float scale, LDS_AS char* buf,
+                                                bf16_t* out, long ld, int nvalid, int lane) {
+  using OT = OutTile<HD>;
+  const int r = lane & 31, hl = lane >> 5;
+#pragma unroll
+  for (int d = 0; d < Hd<HD>::P / 32; ++d)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (d * 32 + 8 * j >= HD) continue;  // head-dim padding (HD is a multiple of 8: wave-uniform)
+      const int c = d * 4 + j;
+      typedef int i32x2 __attribute__((ext_vector_type(2)));
+      i32x2 v;
+      v[0] = (int)pack_bf2(x[d][4 * j] * scale, x[d][4 * j + 1] * scale);
+      v[1] = (int)pack_bf2(x[d][4 * j + 2] * scale, x[d][4 * j + 3] * scale);
+      *(LDS_AS i32x2*)(buf + r * (OT::CH * 16) + ((c ^ (r & OT::SWM)) * 16) + hl * 8) = v;
+    }
+#pragma unroll
+  for (int i0 = 0; i0 < 32 * OT::NCH; i0 += 64) {
+    const int i = i0 + lane;
+    const int row = i / OT::NCH, c = i - row * OT::NCH;
+    if ((32 * OT::NCH) % 64 == 0 || i < 32 * OT::NCH) {
+      const i32x4 v = *(const LDS_AS i32x4*)(buf + row * (OT::CH * 16) + ((c ^ (row & OT::SWM)) * 16));
+      if (row < nvalid) *(i32x4*)(out + (long)row * ld + c * 8) = v;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Forward: block = 4 waves x 32 queries, KV tiles of 64 keys double-buffered in LDS.
 template <int HD>
@@ -457,17 +497,22 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
   }
   const float l_tot = sum_xor32(lsum);
   const float inv = 1.f / l_tot;
-  if (qok) {
-    bf16_t* orow = a.o + (long)(seq0 + qloc) * a.ldo + h * HD;
+  if constexpr (HD == 32) {
+    // head dim 32 (5 workgroups per CU): the direct 4-B stores measured faster than the LDS image
+    // (predictor forward 269 vs 278 us, profiles/r05_attn_row_stores_ab.txt)
+    if (qok) {
+      bf16_t* orow = a.o + (long)(seq0 + qloc) * a.ldo + h * HD;
 #pragma unroll
-    for (int d = 0; d < HDP / 32; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int col = d * 32 + acc_row(r, lane);
-        if (col < HD) *(uint32_t*)(orow + col) = pack_bf2(ot[d][r] * inv, ot[d][r + 1] * inv);
-      }
-    if (hl == 0) a.stats[(long)h * a.T + seq0 + qloc] = m_use * c + __log2f(l_tot);  // log2 units
+      for (int r = 0; r < 16; r += 2) *(uint32_t*)(orow + acc_row(r, lane)) = pack_bf2(ot[0][r] * inv, ot[0][r + 1] * inv);
+    }
+  } else {
+    // the K / V buffers are free after the last tile's barrier
+    static_assert(4 * OutTile<HD>::BYTES <= 4 * TB, "output images fit the K / V buffers");
+    const int q0 = qt * 128 + wave * 32;
+    wave_store_rows<HD>(ot, inv, smem + wave * OutTile<HD>::BYTES, a.o + (long)(seq0 + q0) * a.ldo + h * HD, a.ldo,
+                        len - q0, lane);
   }
+  if (qok && hl == 0) a.stats[(long)h * a.T + seq0 + qloc] = m_use * c + __log2f(l_tot);  // log2 units
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -481,7 +526,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   constexpr int TB = QT * HDP * 2;
   // per stage: Q tile, dO tile, 32 lse + 32 delta floats
   constexpr int STAGE = 2 * TB + 256;
-  __shared__ __attribute__((aligned(16))) char smem_raw[2 * STAGE];
+  constexpr int SMEM = 2 * STAGE > 4 * OutTile<HD>::BYTES ? 2 * STAGE : 4 * OutTile<HD>::BYTES;
+  __shared__ __attribute__((aligned(16))) char smem_raw[SMEM];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int tile_id, h;
@@ -643,13 +689,14 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
     tile_iter(qt0, std::integral_constant<int, 0>{});
     if (qt0 + 1 < nqt) tile_iter(qt0 + 1, std::integral_constant<int, 1>{});
   }
+  // the Q / dO buffers are free after the last tile's barrier: rows go out through a wave-private image
+  LDS_AS char* ob = smem + wave * OutTile<HD>::BYTES;
 #pragma unroll
   for (int kw = 0; kw < KW; ++kw) {
-    if (!kok[kw]) continue;
-    bf16_t* dk = a.dqkv + (long)(seq0 + kloc[kw]) * a.ldd + a.k_off + h * HD;
-    bf16_t* dv = a.dqkv + (long)(seq0 + kloc[kw]) * a.ldd + a.v_off + h * HD;
+    const int k0 = kt * 128 * KW + kw * 128 + wave * 32;
+    if (k0 >= len) continue;  // wave-uniform
     const bool rope = a.cos_t != nullptr;
-    const TokPos tp = rope ? tok_pos(a, seq0 + kloc[kw]) : TokPos{0, 0, 0};
+    const TokPos tp = rope ? tok_pos(a, seq0 + min(kloc[kw], len - 1)) : TokPos{0, 0, 0};
     // rotate everything before the first store (the stores could alias the tables, so the
     // table loads would otherwise be serialised behind them)
 #pragma unroll
@@ -657,15 +704,9 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) dkt[kw][d][r] *= a.scale;
     if (rope) rope_inv_rows<HD>(a, tp, lane, dkt[kw]);
-#pragma unroll
-    for (int d = 0; d < HDP / 32; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int col = d * 32 + acc_row(r, lane);
-        if (col >= HD) continue;
-        *(uint32_t*)(dk + col) = pack_bf2(dkt[kw][d][r], dkt[kw][d][r + 1]);
-        *(uint32_t*)(dv + col) = pack_bf2(dvt[kw][d][r], dvt[kw][d][r + 1]);
-      }
+    const long row0 = (long)(seq0 + k0) * a.ldd + h * HD;
+    wave_store_rows<HD>(dkt[kw], 1.f, ob, a.dqkv + row0 + a.k_off, a.ldd, len - k0, lane);
+    wave_store_rows<HD>(dvt[kw], 1.f, ob, a.dqkv + row0 + a.v_off, a.ldd, len - k0, lane);
   }
 }
 
@@ -831,24 +872,22 @@ __global__ __launch_bounds__(256, (HD == 64 ? DQ64_OCC : 1)) void k_attn_bwd_dq(
     tile_iter(kt0, std::integral_constant<int, 0>{});
     if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
   }
+  // the K / V buffers are free after the last tile's barrier: rows go out through a wave-private image
+  static_assert(4 * OutTile<HD>::BYTES <= 4 * TB, "output images fit the K / V buffers");
+  LDS_AS char* ob = smem + wave * OutTile<HD>::BYTES;
 #pragma unroll
   for (int qw = 0; qw < QW; ++qw) {
-    if (!qok[qw]) continue;
-    bf16_t* dq = a.dqkv + (long)(seq0 + qloc[qw]) * a.ldd + a.q_off + h * HD;
+    const int q0 = qt * 128 * QW + qw * 128 + wave * 32;
+    if (q0 >= len) continue;  // wave-uniform
     const bool rope = a.cos_t != nullptr;
-    const TokPos tp = rope ? tok_pos(a, seq0 + qloc[qw]) : TokPos{0, 0, 0};
+    const TokPos tp = rope ? tok_pos(a, seq0 + min(qloc[qw], len - 1)) : TokPos{0, 0, 0};
 #pragma unroll
     for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dqt[qw][d][r] *= a.scale;
     if (rope) rope_inv_rows<HD>(a, tp, lane, dqt[qw]);  // rotate first, then store (see k_attn_bwd_dkdv)
-#pragma unroll
-    for (int d = 0; d < HDP / 32; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int col = d * 32 + acc_row(r, lane);
-        if (col < HD) *(uint32_t*)(dq + col) = pack_bf2(dqt[qw][d][r], dqt[qw][d][r + 1]);
-      }
+    wave_store_rows<HD>(dqt[qw], 1.f, ob, a.dqkv + (long)(seq0 + q0) * a.ldd + a.q_off + h * HD, a.ldd, len - q0,
+                        lane);
   }
 }
 

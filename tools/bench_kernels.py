@@ -73,6 +73,8 @@ ATTN = [("attn fwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], False),
         ("attn bwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], True),
         ("attn fwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], False),
         ("attn bwd hd32 pred", 32, 12, [(24, 1464), (24, 1504)], True),
+        ("attn bwd hd64 ctx rope", 64, 16, [(24, 424), (24, 64)], "rope"),
+        ("attn bwd hd32 pred rope", 32, 12, [(24, 1464), (24, 1504)], "rope"),
         ("attn fwd hd64 N2048", 64, 16, [(8, 2048)], False),
         ("attn bwd hd64 N2048", 64, 16, [(8, 2048)], True),
         ("attn bwd hd64 N4608", 64, 16, [(2, 4608)], True),
@@ -154,9 +156,16 @@ def attn_case(lib, hd, H, groups, dev, stream, bwd):
         assert lib.vj_attn_fwd(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(stats), sc, len(groups), ns, ln, stream) == 0
     fwd()
 
+    # bwd == "rope": with the inverse 3-axis RoPE fused into the dq / dk stores (as the step runs it)
+    half = (hd // 3) // 2
+    tab = torch.rand(256 * half, device=dev) * 6.0
+    cos_t, sin_t = tab.cos(), tab.sin()
+    rope = (None, max(g[1] for g in groups), 64, 8, P(cos_t), P(sin_t)) if bwd == "rope" else (None, 0, 0, 0, None, None)
+
     def bwdf():
         assert lib.vj_attn_bwd(T, H, hd, P(qkv), 3 * D, 0, D, 2 * D, P(o), D, P(do), D, P(stats), P(dqkv), 3 * D,
-                               sc, len(groups), ns, ln, None, 0, 0, 0, None, None, stream) == 0
+                               sc, len(groups), ns, ln, *rope, stream) == 0
+    bwdf.keep = (cos_t, sin_t)  # the tables stay allocated while the case runs
     fl = sum(4.0 * n * l * l * D for n, l in groups)
     return (bwdf, 2.5 * fl) if bwd else (fwd, fl)  # backward: FA2 convention, 5 matmuls
 

@@ -22,4 +22,5 @@ echo "pmc ok"
 # the bench's own dominant kernel (roofline.kernel of its JSON line)
 dom=$(python3 -c "import json,sys; print(json.loads([l for l in open('$out/bench.log') if l.startswith('{')][-1])['roofline']['kernel'])")
 echo "dominant: $dom"
+cp profiles/traffic.json "$out/traffic.json"  # merged: this entry replaced, the ViT-g entries kept
 python3 tools/traffic.py gpurun_out/pmc_bench/$tag/p2 gpurun_out/pmc_bench/$tag/p3 "$dom" "$out/traffic.json"

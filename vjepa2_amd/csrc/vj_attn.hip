@@ -372,12 +372,9 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
 #pragma unroll
     for (int d = 0; d < HDP / 32; ++d) ot[d][r] = 0.f;
   // Lazy rescaling: p = exp2(c*s - c*m_use) with m_use the raw-score max seen when O was last
-  // rescaled; O is rescaled (wave-uniform branch) only when some query's max grows by more than
-  // TAU/c, so p <= 2^TAU stays well inside fp32/bf16 range. The result is invariant to m_use.
-  constexpr float TAU = 8.f;
+  // rescaled (the deferred-max rule below); the result is invariant to m_use.
   float m_use = -INFINITY, cm = 0.f;
   const float c = a.scale * LOG2E;
-  const float tau = TAU / c;
 
   // per-lane V^T read addresses (tr_frag_at): LDS base + lane part, d = column block
   uint32_t vlo[HDP / 32], vhi[HDP / 32];
@@ -396,48 +393,28 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
   constexpr bool PRIO_PV = HD == 64;
   // loop body with the LDS buffer index as a compile-time constant (unrolled by 2), so every LDS
   // address is a per-lane base register plus an immediate offset
-  auto tile_iter = [&](const int kt, auto cur_c) {
-    constexpr int cur = decltype(cur_c)::value;
-    const LDS_AS char* Ks = smem + cur * 2 * TB;
-    const LDS_AS char* Vs = Ks + TB;
-    if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
-      LDS_AS char* nx = smem + (cur ^ 1) * 2 * TB;
-      stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
-      stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
-    }
-    f32x16 st[2];
+  // S^T = K Q^T of the tile's two 32-key halves (kf: the K fragments, all read before the MFMAs)
+  auto s_tile = [&](const LDS_AS char* Ks, f32x16 (&st)[2]) {
+    bf16x8 kf[2][HDP / 16];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int s = 0; s < HDP / 16; ++s) kf[kk][s] = row_frag<HDP>(Ks, kk * 32, s, lane);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[kk][r] = 0.f;
-    constexpr int VIMG = cur * 2 * TB + TB;
-    bf16x8 vf[4][HDP / 32];
-    {
-      // all K fragments first (one LDS wait), then two independent S^T chains interleaved
-      bf16x8 kf[2][HDP / 16];
+    if (PRIO_S) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < HDP / 16; ++s)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int s = 0; s < HDP / 16; ++s) kf[kk][s] = row_frag<HDP>(Ks, kk * 32, s, lane);
-      if (PRIO_S) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int s = 0; s < HDP / 16; ++s)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][s], qf[s], st[kk], 0, 0, 0);
-      if (PRIO_S) __builtin_amdgcn_s_setprio(0);
-      // V^T fragments: issued before the softmax so their LDS latency hides under it (per-lane base
-      // registers + immediates: the buffer and the k-step are compile-time)
-#pragma unroll
-      for (int d = 0; d < HDP / 32; ++d) {
-        vf[0][d] = tr_frag_at<HDP, VIMG, 0>(vlo[d], vhi[d]);
-        vf[1][d] = tr_frag_at<HDP, VIMG, 16>(vlo[d], vhi[d]);
-        vf[2][d] = tr_frag_at<HDP, VIMG, 32>(vlo[d], vhi[d]);
-        vf[3][d] = tr_frag_at<HDP, VIMG, 48>(vlo[d], vhi[d]);
-      }
-    }
-    const int kb = kt * KT;
-    if (kb + KT > kmask0) {  // ragged last tile (or frame-causal boundary tiles): keys past the limit get -inf
+        st[kk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][s], qf[s], st[kk], 0, 0, 0);
+    if (PRIO_S) __builtin_amdgcn_s_setprio(0);
+  };
+  // keys past the limit get -inf (ragged last tile, frame-causal boundary tiles)
+  auto mask_tile = [&](const int kb, f32x16 (&st)[2]) {
+    if (kb + KT > kmask0) {
       asm volatile("");  // keeps the compiler from if-converting this into every tile
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -445,36 +422,84 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
         for (int r = 0; r < 16; ++r)
           if (kb + kk * 32 + acc_row(r, lane) >= klim) st[kk][r] = -INFINITY;
     }
+  };
+  // m_use := the running row max (exact), O and l rescaled to it
+  auto to_row_max = [&](const f32x16 (&st)[2]) {
     float mx = st[0][0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, st[0][r]);
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[1][r]);
     mx = max_xor32(mx);
-    if (__builtin_amdgcn_ballot_w64(mx > m_use + tau)) {
-      asm volatile("");  // a real (rare) branch, not if-converted into every tile
-      const float m_new = fmaxf(m_use, mx);
-      const float alpha = __builtin_amdgcn_exp2f((m_use - m_new) * c);
-      m_use = m_new;
-      cm = m_new * c;
+    const float m_new = fmaxf(m_use, mx);
+    const float alpha = __builtin_amdgcn_exp2f((m_use - m_new) * c);
+    m_use = m_new;
+    cm = m_new * c;
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
+    for (int r = 0; r < 16; ++r)
 #pragma unroll
-        for (int d = 0; d < HDP / 32; ++d) ot[d][r] *= alpha;
-      lsum *= alpha;
-    }
+      for (int d = 0; d < HDP / 32; ++d) ot[d][r] *= alpha;
+    lsum *= alpha;
+  };
+  // p = 2^(c s - c m_use) in place; returns this lane's sum of its 32 p (two partial chains)
+  auto exp_tile = [&](f32x16 (&st)[2]) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[kk][r] = __builtin_amdgcn_exp2f(fmaf(st[kk][r], c, -cm));
-    // two partial chains keep the adds off one dependency path
     float ls0 = st[0][0], ls1 = st[1][0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) {
       ls0 += st[0][r];
       ls1 += st[1][r];
     }
-    lsum += ls0 + ls1;
+    return ls0 + ls1;
+  };
+  // Deferred max (round 5): after the first tile the exponentials are taken against the running m_use
+  // without the tile's row max (24 of ~140 VALU per tile); the lane's p sum bounds every p, so while
+  // no lane's sum exceeds PLIM every p <= PLIM (range-safe in f32 / bf16, and the result does not
+  // depend on m_use). A lane over the bound (a max that grew, an overflow, a NaN) sends the wave down
+  // the exact path: S recomputed from the K tile (still in LDS) and Q, row max, rescale, exponentials.
+  constexpr float PLIM = 4096.f;
+  // loop body with the LDS buffer index as a compile-time constant (unrolled by 2), so every LDS
+  // address is a per-lane base register plus an immediate offset
+  auto tile_iter = [&](const int kt, auto cur_c, auto first_c) {
+    constexpr int cur = decltype(cur_c)::value;
+    constexpr bool FIRST = decltype(first_c)::value;
+    const LDS_AS char* Ks = smem + cur * 2 * TB;
+    if (kt + 1 < nkt) {  // next tile's DMA: lands during this whole iteration
+      LDS_AS char* nx = smem + (cur ^ 1) * 2 * TB;
+      stage_rows<HD, KT>(rk, a.ld, (kt + 1) * KT, len, nx, wave, lane, 4);
+      stage_rows<HD, KT>(rv, a.ld, (kt + 1) * KT, len, nx + TB, wave, lane, 4);
+    }
+    f32x16 st[2];
+    s_tile(Ks, st);
+    // V^T fragments: issued before the softmax so their LDS latency hides under it (per-lane base
+    // registers + immediates: the buffer and the k-step are compile-time)
+    constexpr int VIMG = cur * 2 * TB + TB;
+    bf16x8 vf[4][HDP / 32];
+#pragma unroll
+    for (int d = 0; d < HDP / 32; ++d) {
+      vf[0][d] = tr_frag_at<HDP, VIMG, 0>(vlo[d], vhi[d]);
+      vf[1][d] = tr_frag_at<HDP, VIMG, 16>(vlo[d], vhi[d]);
+      vf[2][d] = tr_frag_at<HDP, VIMG, 32>(vlo[d], vhi[d]);
+      vf[3][d] = tr_frag_at<HDP, VIMG, 48>(vlo[d], vhi[d]);
+    }
+    const int kb = kt * KT;
+    mask_tile(kb, st);
+    if constexpr (FIRST) to_row_max(st);
+    float ls = exp_tile(st);
+    if constexpr (!FIRST) {
+      if (__builtin_amdgcn_ballot_w64(!(ls <= PLIM))) {
+        asm volatile("");  // a real (rare) branch, not if-converted into every tile
+        lds_wait();        // the V reads in flight complete first (LDS returns in order)
+        s_tile(Ks, st);
+        mask_tile(kb, st);
+        to_row_max(st);
+        ls = exp_tile(st);
+      }
+    }
+    lsum += ls;
     // O^T += V^T P^T over 4 key-steps of 16
     lds_wait();
     {
@@ -491,9 +516,12 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
     }
     __syncthreads();
   };
-  for (int kt0 = 0; kt0 < nkt; kt0 += 2) {
-    tile_iter(kt0, std::integral_constant<int, 0>{});
-    if (kt0 + 1 < nkt) tile_iter(kt0 + 1, std::integral_constant<int, 1>{});
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  tile_iter(0, I0{}, std::true_type{});
+  for (int kt0 = 1; kt0 < nkt; kt0 += 2) {
+    tile_iter(kt0, I1{}, std::false_type{});
+    if (kt0 + 1 < nkt) tile_iter(kt0 + 1, I0{}, std::false_type{});
   }
   const float l_tot = sum_xor32(lsum);
   const float inv = 1.f / l_tot;

@@ -200,8 +200,18 @@ class Block(nn.Module):
             raise NotImplementedError("attn_mask is not supported on the HIP path")
         B, N, C = x.shape
         lay = self.layout_for(B, N, mask, T, H_patches, W_patches, x.device)
-        y = fn.run_block(x.float().reshape(B * N, C).contiguous(), self, lay)
+        y = fn.run_block(_residual_rows(x, self), self, lay)
         return y.reshape(B, N, C)
+
+
+def _residual_rows(x, blk):
+    """The block's residual stream in the input's dtype, as under the reference's autocast: a bf16 x
+    stays bf16 (x + attn(norm1(x)) is a bf16 add, modules.py:561-562, and the block returns bf16), an
+    f32 x stays f32. An active drop_path in training keeps f32 (not built on the bf16 stream)."""
+    rows = x.reshape(-1, x.shape[-1]).contiguous()
+    if rows.dtype == torch.bfloat16 and not (getattr(blk.drop_path, "drop_prob", 0.0) and blk.drop_path.training):
+        return rows
+    return rows.float()
 
 
 def build_action_block_causal_attention_mask(T, H, W, add_tokens=1):
@@ -285,7 +295,7 @@ class ACBlock(nn.Module):
             if attn_mask is not None:
                 raise NotImplementedError("attn_mask without RoPE is not on the AC predictor path")
             lay = fn.TokenLayout([(B, N)], ids=None, ids_mod=N)
-        return fn.run_block(x.float().reshape(B * N, C).contiguous(), self, lay).reshape(B, N, C)
+        return fn.run_block(_residual_rows(x, self), self, lay).reshape(B, N, C)
 
 
 class CrossAttention(nn.Module):

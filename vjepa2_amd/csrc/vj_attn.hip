@@ -275,18 +275,6 @@ __device__ __forceinline__ bf16x8 acc_frag(const f32x16& a, int s) {
   return v;
 }
 
-// Backward operand prescale: the register-resident S operand (K in the dK/dV sweep, Q in the dQ sweep)
-// times c = scale * log2(e), rounded to bf16 once per block, so the MFMA yields c*S and the softmax
-// needs no per-score multiply (one VALU op of four per score; both sweeps are bound by vector issue).
-// The rounding of c*k / c*q perturbs c*S by ~2^-9 |S| c / sqrt(hd) (~1e-3 in log2 units on unit-variance
-// rows), under the bf16 rounding P already takes for the dV / dK MFMAs.
-__device__ __forceinline__ bf16x8 scale_frag(const bf16x8 v, float c) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (__bf16)((float)v[j] * c);
-  return r;
-}
-
 __device__ __forceinline__ bf16x8 gload8(const bf16_t* p, bool ok) {
   if (!ok) {
     bf16x8 z;
@@ -595,11 +583,6 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       vf[kw][s] = gload8(vrow + 16 * s + 8 * hl, kok[kw] && 16 * s + 8 * hl < HD);
     }
   }
-  const float c = a.scale * LOG2E;
-#pragma unroll
-  for (int kw = 0; kw < KW; ++kw)
-#pragma unroll
-    for (int s = 0; s < HDP / 16; ++s) kf[kw][s] = scale_frag(kf[kw][s], c);  // S = Q (cK)^T = c Q K^T
   const uint32_t qbytes = (uint32_t)min((long)len * a.ld * 2, 0x7fffffffL);
   const uint32_t dbytes = (uint32_t)min((long)len * a.lddo * 2, 0x7fffffffL);
   const __amdgpu_buffer_rsrc_t rq = make_rsrc(a.qkv + (long)seq0 * a.ld + a.q_off + h * HD, qbytes);
@@ -615,6 +598,8 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
     for (int d = 0; d < HDP / 32; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dvt[kw][d][r] = dkt[kw][d][r] = 0.f;
+  const float c = a.scale * LOG2E;
+  const float rc = -1.f / c;
 
   auto stage = [&](int qt, LDS_AS char* st) {
     stage_rows<HD, QT>(rq, a.ld, qt * QT, len, st, wave, lane, 4);
@@ -660,13 +645,13 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
       qa[s] = row_frag<HDP>(Qs, 0, s, lane);
       da[s] = row_frag<HDP>(Ds, 0, s, lane);
     }
-    // c S - lse2 = Q (cK)^T - lse2 (rows: queries, col: key); dP - delta = dO V^T - delta: the
+    // S - lse2/c = Q K^T - lse2/c (rows: queries, col: key); dP - delta = dO V^T - delta: the
     // per-query terms are the accumulators' initial values, so no per-row registers stay live
     f32x16 sacc[KW], dp[KW];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = acc_row(r, lane);
-      const float l2 = -Ls[qi], dl = Ls[32 + qi];
+      const float l2 = Ls[qi] * rc, dl = Ls[32 + qi];
 #pragma unroll
       for (int kw = 0; kw < KW; ++kw) {
         sacc[kw][r] = l2;
@@ -703,7 +688,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
     for (int kw = 0; kw < KW; ++kw)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(sacc[kw][r]);
+        const float p = __builtin_amdgcn_exp2f(sacc[kw][r] * c);
         sacc[kw][r] = p;
         dp[kw][r] *= p;
       }
@@ -815,13 +800,9 @@ __global__ __launch_bounds__(256, (HD == 64 ? DQ64_OCC : 1)) void k_attn_bwd_dq(
 #pragma unroll
       for (int r = 0; r < 16; ++r) dqt[qw][d][r] = 0.f;
   const float c = a.scale * LOG2E;
-  float nl2[QW];  // -lse2: initial value of the S^T accumulators, so p = 2^acc with S^T = K (cQ)^T
+  float nl2[QW];  // -lse2 / c: initial value of the S^T accumulators, so p = 2^(c * acc)
 #pragma unroll
-  for (int qw = 0; qw < QW; ++qw) {
-    nl2[qw] = -lse2[qw];
-#pragma unroll
-    for (int s = 0; s < HDP / 16; ++s) qf[qw][s] = scale_frag(qf[qw][s], c);
-  }
+  for (int qw = 0; qw < QW; ++qw) nl2[qw] = -lse2[qw] / c;
   // frame-causal key limits (as in the forward)
   int klim[QW];
 #pragma unroll
@@ -899,7 +880,7 @@ __global__ __launch_bounds__(256, (HD == 64 ? DQ64_OCC : 1)) void k_attn_bwd_dq(
 #pragma unroll
       for (int qw = 0; qw < QW; ++qw)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dpt[qw][r] *= __builtin_amdgcn_exp2f(st[qw][r]);
+        for (int r = 0; r < 16; ++r) dpt[qw][r] *= __builtin_amdgcn_exp2f(st[qw][r] * c);
       lds_wait();
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) tie(ktf[s2]);

@@ -275,6 +275,9 @@ def test_attention_f32_parity_mode(hd, H, groups):
     _close(lse, lse_ref, 2e-6, 2e-6, f"attn f32 lse hd={hd}")
 
 
+SPIKE_BWD_REL = 1.0e-2
+
+
 @pytest.mark.parametrize("hd", [64, 32, 80])
 def test_attention_rescale_spikes(hd):
     """Score maxima that grow tile after tile (every step takes the lazy-rescale branch) and one
@@ -296,11 +299,24 @@ def test_attention_rescale_spikes(hd):
     qkv = qkv.to(DEV).bfloat16()
     scale = hd ** -0.5
     o, stats = ops.attn_fwd(qkv, H, hd, groups, scale)
-    q, k, v = (qkv[:, i * D:(i + 1) * D].float().reshape(T, H, hd) for i in range(3))
+    q, k, v = (qkv[:, i * D:(i + 1) * D].float().reshape(T, H, hd).requires_grad_(True) for i in range(3))
     o_ref, lse_ref = _attn_ref(q, k, v, groups, scale)
     torch.cuda.synchronize()
     _close(o.reshape(T, H, hd), o_ref, 1e-2, 2e-2, f"attn spikes fwd hd={hd}")
     _close(stats[0] * math.log(2.0), lse_ref, 2e-3, 1e-4, f"attn spikes lse hd={hd}")
+    # the backward on the same large, growing logits (the spike key's score is ~8 |q|^2)
+    do = torch.randn(T, D, generator=g).to(DEV).bfloat16()
+    o_ref.backward(do.float().reshape(T, H, hd))
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, groups, scale)
+    torch.cuda.synchronize()
+    # elementwise bounds do not fit here (dq of the spike rows is large; P and dS are bf16 MFMA
+    # operands), so the bound is on the relative L2 error of each gradient
+    for i, (name, t) in enumerate((("dq", q), ("dk", k), ("dv", v))):
+        got = dqkv[:, i * D:(i + 1) * D].reshape(T, H, hd).float().cpu()
+        exp = t.grad.float().cpu()
+        rel = ((got - exp).norm() / exp.norm()).item()
+        print(f"attn spikes {name} hd={hd}: relative L2 error {rel:.3e}")
+        assert rel < SPIKE_BWD_REL, (name, hd, rel)
 
 
 # ------------------------------------------------------------------------------------------------

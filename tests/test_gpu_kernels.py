@@ -58,11 +58,12 @@ def test_gemm_layouts(a_kmajor, b_kmajor, shape):
     _close(out, exp, 1e-4 * math.sqrt(K) * 4, 1e-4, f"gemm {shape} ak={a_kmajor} bk={b_kmajor}")
 
 
-@pytest.mark.parametrize("MNK", [(200, 136, 3000), (520, 392, 3000), (512, 256, 4100)])
+@pytest.mark.parametrize("MNK", [(200, 136, 3000), (520, 392, 3000), (512, 256, 4100), (600, 1408, 2000)])
 @pytest.mark.parametrize("epi", [1, 2, 0])
 def test_gemm_splitk(epi, MNK):
     """Deterministic split-K (weight-gradient shape: small M x N, K = tokens). M >= 256 and N >= 128
-    take the 256-row-tile partial kernel (BN 128 / 256), the first shape the 128-tile one."""
+    take the 256-row-tile partial kernel (BN 128 / 256; N = 1408: 256-wide tiles with a half-empty
+    last one, ViT-g's width), the first shape the 128-tile one."""
     from vjepa2_amd import ops
 
     g = torch.Generator(device="cpu").manual_seed(epi)

@@ -56,6 +56,13 @@ GEMMS = [
     ("wgrad fc1", 4096, 1024, 11712, 0, 0, 2, 4),
     ("wgrad qkv", 3072, 1024, 11712, 0, 0, 2, 5),
     ("wgrad proj", 1024, 1024, 11712, 0, 0, 2, 15),
+    # ViT-g (D = 1408) weight gradients, K = 34304 context tokens: split 4 / 5 / 6 (the 128- and
+    # 256-wide column-tile sizings pick different splits)
+    ("g wgrad qkv s4", 4224, 1408, 34304, 0, 0, 2, 4),
+    ("g wgrad qkv s5", 4224, 1408, 34304, 0, 0, 2, 5),
+    ("g wgrad fc1 s6", 6144, 1408, 34304, 0, 0, 2, 6),
+    ("g wgrad fc1 s5", 6144, 1408, 34304, 0, 0, 2, 5),
+    ("g wgrad proj s7", 1408, 1408, 34304, 0, 0, 2, 7),
     ("pred qkv", 71232, 1152, 384, 1, 1, 0, 1),
     ("pred dgrad fc1", 71232, 384, 1536, 1, 0, 0, 1),
     ("pred wgrad fc1", 1536, 384, 71232, 0, 0, 2, 14),

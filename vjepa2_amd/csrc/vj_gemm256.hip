@@ -1186,6 +1186,10 @@ int launch256(int epi, const G256& g, hipStream_t st) {
 
 }  // namespace
 
+// 256-wide column tiles unless the last one would waste more than 15 % of the work (measured,
+// tools/bench_kernels.py: predictor QKV N = 1152 -17 % with 256-wide tiles; N = 384 +14 %)
+bool wide_tile_ok(int N) { return N % 256 == 0 || (N > 256 && vj_cdiv(N, 256) * 256L * 100 <= 115L * N); }
+
 // Called by vj_gemm_bf16_splitk (splitk == 1) when the problem suits a 256-row tile; arguments
 // already validated there. Returns VJ_ERR_UNSUPPORTED when it declines.
 int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
@@ -1195,10 +1199,7 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
     return VJ_ERR_UNSUPPORTED;
   if (((uintptr_t)C & 15) || ((uintptr_t)C2 & 15) || ((uintptr_t)aux & 15) || ((uintptr_t)bias & 15))
     return VJ_ERR_UNSUPPORTED;
-  // 256-wide tiles (direct-store epilogue) unless the last column tile would waste > 15 % of the work
-  // (measured, tools/bench_kernels.py: predictor QKV N = 1152 -17 % with 256-wide tiles; N = 384 +14 %)
-  const bool wide = N % 256 == 0 || (N > 256 && vj_cdiv(N, 256) * 256L * 100 <= 115L * N);
-  const int bn = wide ? 256 : 128;
+  const int bn = wide_tile_ok(N) ? 256 : 128;  // direct-store epilogue on the 256-wide tiles
   const int tm = vj_cdiv(M, 256), tn = vj_cdiv(N, bn);
   G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, C, ldc, C2, ldc2, bias, aux, ldaux,
          tm, tn, RopeP{}, K, 1, nullptr, tile_group(tm, tn)};
@@ -1235,7 +1236,9 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
 int vj_gemm256_partial(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
                        int b_kmajor, int kslice, int splitk, float* ws, hipStream_t st) {
   if (a_kmajor || b_kmajor || N % 8 || M < 256 || N < 128) return VJ_ERR_UNSUPPORTED;
-  const int bn = (N % 256 == 0) ? 256 : 128;
+  // 256-wide tiles unless the last one would waste more than 15 % of the columns (the forward GEMMs'
+  // rule): ViT-g's N = 1408 runs 6 tiles of 256 instead of 11 of 128 (twice the work per operand byte)
+  const int bn = wide_tile_ok(N) ? 256 : 128;
   const int tm = vj_cdiv(M, 256), tn = vj_cdiv(N, bn);
   if ((long)tm * tn * splitk > 0x7fffffffL) return VJ_ERR_UNSUPPORTED;
   G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,

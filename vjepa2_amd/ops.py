@@ -120,8 +120,9 @@ def wgrad_splitk(M, N, K, cus=None):
     stream configuration (tests/test_gpu_production.py)."""
     if cus is None:
         cus = 256
-    if M >= 256 and N >= 128:
-        tm, tn, per_cu = 256, (256 if N % 256 == 0 else 128), 1
+    if M >= 256 and N >= 128:  # the C side's column-tile rule (vj_gemm256.hip wide_tile_ok)
+        wide = N % 256 == 0 or (N > 256 and -(-N // 256) * 256 * 100 <= 115 * N)
+        tm, tn, per_cu = 256, (256 if wide else 128), 1
     else:
         tm, tn, per_cu = 128, 128, 2
     tiles = -(-M // tm) * -(-N // tn)

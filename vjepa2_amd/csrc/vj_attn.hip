@@ -33,7 +33,12 @@
 // softmax, priority around the backward MFMAs, the fused backward (dQ partials from the dK/dV sweep
 // plus a reduce pass; 192.7 vs 196.9 clips/s) and a separate delta kernel.
 constexpr int KW32 = 2, QW32 = 2, KW64 = 1, QW64 = 1;
-constexpr int FWD_OCC = 3;    // forward workgroups per CU the register budget is sized for (hd <= 64)
+// Forward occupancy hint (hd <= 64): the launch bound asks for 2 waves per SIMD, but the kernel compiles
+// to 160 VGPRs (hd 64) / 94 (hd 32) and runs 3 / 5 per SIMD; with the bound at 3 the register allocator
+// lands on 166 and a different schedule: target forward 425.7 -> 415.7 us, N = 8192 725 -> 717 us
+// with this bound (profiles/r05_attn_fwd_occ_kernels.txt). Keep an eye on the VGPR count: above 168
+// the hd-64 forward would drop to 2 waves per SIMD.
+constexpr int FWD_OCC = 2;
 constexpr int DQ64_OCC = 3;   // dQ sweep, head dim 64: 168 VGPRs (one dword reloaded per key tile)
 
 namespace {

@@ -219,7 +219,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = (4 * (wave & 3) + j) * 16 + (lane >> 2);  // LDS row of the lane's 16-B chunk
-        const int c = (lane & 3) ^ ((r >> 2) & 3);              // its logical chunk (64-B row swizzle)
+        const int c = (lane & 3) ^ kswz32(r);                   // its logical chunk (64-B row swizzle)
         int gr = r;
         if (!isA) {  // PERM (stage()): LDS row r of a 64-row group holds group row 4 (r % 16) + r / 16
           const int rl = r & 63;

@@ -10,7 +10,8 @@ def main(d):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")[:60]
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+            name = (name[5:] if name.startswith("void ") else name).split("(")[0][:70]
             acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for name, cs in acc.items():
         print(name)

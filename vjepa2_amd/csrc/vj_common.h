@@ -122,8 +122,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc((void*)(lo | (hi << 32)), (short)0, n, 0x00020000);
 }
 // 16 bytes per lane, global(rsrc + voffset) -> LDS(lds_wave_base + lane*16). Out-of-range -> zeros.
+#ifndef VJ_DMA_CPOL
+#define VJ_DMA_CPOL 0
+#endif
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, LDS_AS void* lds_wave_base, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_wave_base, 16, voff, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, lds_wave_base, 16, voff, 0, 0, VJ_DMA_CPOL);
 }
 #define VJ_OOB 0x80000000u
 

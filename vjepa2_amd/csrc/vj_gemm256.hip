@@ -53,6 +53,13 @@ __device__ long vj_gemm_stamps[2048 * 16 * 4];
 // BMT = 192 (8-wave, K-major bf16, 256-wide direct-store tiles only): 96-row wave tiles (3 m-tiles
 // per M-half) for problems whose 256-row tile count leaves a round of CUs under-filled (context
 // GEMMs, M ~ 11.7k: 184 tiles of 256 x 256 on 256 CUs -> 244 tiles of 192 x 256).
+// VJ_STG_CPOL: cache-policy bits of the staggered loop's LDS-DMA pieces (0; sc1 = 16 measured within
+// noise, nt = 2 up to 2x slower). VJ_DIAG_NODMA / NOWAIT / SAMEADDR / FULL128: timing-only builds that
+// compute WRONG results (no DMA after the prologue; relaxed unit wait; every piece from one 1-KB block;
+// pieces of 8 whole 128-B rows) - profiles/r05_gemm_dma_diag.txt, never in the shipped library.
+#ifndef VJ_STG_CPOL
+#define VJ_STG_CPOL 0
+#endif
 template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, bool STG = false>
 __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   static_assert(!STG || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256 && EPI != EPI_PARTIAL),
@@ -226,6 +233,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           gr = (r - rl) + 4 * (rl & 15) + (rl >> 4);
         }
         dvo[j] = gr < left ? (uint32_t)(gr * ld * 2 + c * 16) : VJ_OOB;
+#if VJ_DIAG_FULL128
+        dvo[j] = (uint32_t)(((4 * (wave & 3) + j) * 8 + (lane >> 3)) * ld * 2 + (lane & 7) * 16);
+#endif
+#if VJ_DIAG_SAMEADDR
+        dvo[j] = (uint32_t)(lane * 16);
+#endif
       }
     } else {
 #pragma unroll
@@ -236,9 +249,18 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   auto dma_half = [&](auto h_c) {
     constexpr int h = decltype(h_c)::value;
     LDS_AS char* dst = ring + (dpos % NSL) * USZ + (isA ? 0 : 16384) + (4 * (wave & 3) + 2 * h) * 1024;
+#if VJ_DIAG_FULL128
+    const int soff = __builtin_amdgcn_readfirstlane((dku >> 1) * 128 + (dku & 1) * 128 * (int)(isA ? g.lda : g.ldb) * 2);
+#else
     const int soff = __builtin_amdgcn_readfirstlane(dku * 64);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst, 16, dvo[2 * h], soff, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst + 1024, 16, dvo[2 * h + 1], soff, 0, 0);
+#endif
+#if VJ_DIAG_NODMA
+    if (dpos < DIST)
+#endif
+    {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst, 16, dvo[2 * h], soff, 0, VJ_STG_CPOL);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, dst + 1024, 16, dvo[2 * h + 1], soff, 0, VJ_STG_CPOL);
+    }
     if constexpr (h == 1) {
       ++dpos;
       if (++dku == nku) {
@@ -467,8 +489,12 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           if constexpr (DIST == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else {
+#if VJ_DIAG_NOWAIT
+          asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+#else
           if constexpr (DIST == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
           else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#endif
         }
         if (AUX && u == nku - 2) stg_aux();
         if (AUX && nku == 1) stg_aux();

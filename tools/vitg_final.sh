@@ -19,7 +19,7 @@ run() {  # name workload bench-args...
     VJ_TGT_STREAM=0 VJ_WGRAD_STREAM=0 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $p -d "$out/${name}_p$i" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 --kernel-events 0 --synced-steps 0 "$@" > "$out/${name}_p$i.log" 2>&1 || { echo "$name pmc $p failed"; tail -3 "$out/${name}_p$i.log"; return 4; }
   done
   python3 tools/traffic.py "$out/${name}_p1" "$out/${name}_p2" "$dom" profiles/traffic.json "$wl" || return 5
-  timeout -k 10 400 python -u bench.py --steps 3 --warmup 2 --cpu-baseline 0 "$@" > "$out/${name}_final.log" 2>&1 || { echo "$name final failed"; return 3; }
+  timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --cpu-baseline 0 "$@" > "$out/${name}_final.log" 2>&1 || { echo "$name final failed"; return 3; }
   grep '^{' "$out/${name}_final.log" | tail -1 > "$out/${name}.json"
   cut -c1-600 "$out/${name}.json"
 }

@@ -31,7 +31,7 @@ def load(path):
     return lib
 
 
-# (name, M, N, K, a_kmajor, b_kmajor, epi, splitk)
+# (name, M, N, K, a_kmajor, b_kmajor, epi, splitk); epi 7 = GELU with GELU' saved, 8 = bf16 residual
 GEMMS = [
     ("square4096", 4096, 4096, 4096, 1, 1, 1, 1),
     ("qkv  ctx", 11712, 3072, 1024, 1, 1, 0, 1),
@@ -46,6 +46,10 @@ GEMMS = [
     ("proj tgt bf16", 49152, 1024, 1024, 1, 1, 0, 1),
     ("fc2  tgt", 49152, 1024, 4096, 1, 1, 2, 1),
     ("fc2  tgt bf16", 49152, 1024, 4096, 1, 1, 0, 1),
+    ("proj tgt bres", 49152, 1024, 1024, 1, 1, 8, 1),  # 8: bf16 residual (the step's proj / fc2)
+    ("fc2  tgt bres", 49152, 1024, 4096, 1, 1, 8, 1),
+    ("proj ctx bres", 11712, 1024, 1024, 1, 1, 8, 1),
+    ("fc2  ctx bres", 11712, 1024, 4096, 1, 1, 8, 1),
     ("dgrad fc2 Wt", 11712, 4096, 1024, 1, 1, 0, 1),
     ("dgrad fc2 GELU_BWD Wt", 11712, 4096, 1024, 1, 1, 4, 1),
     ("pred dgrad fc2 GELU_BWD Wt", 71232, 1536, 384, 1, 1, 4, 1),
@@ -92,7 +96,7 @@ ATTN = [("attn fwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], False),
 def gemm_case(lib, case, dev, stream):
     name, M, N, K, akm, bkm, epi, sk = case
     save_d = epi == 7
-    epi = 3 if save_d else epi
+    epi = 3 if save_d else (7 if epi == 8 else epi)  # 8: EPI_BF16_RESID (7 in the library)
     g = torch.Generator(device="cpu").manual_seed(0)
     A = ((torch.rand(M, K, generator=g) * 2 - 1) if akm else (torch.rand(K, M, generator=g) * 2 - 1)).to(dev).bfloat16()
     B = ((torch.rand(N, K, generator=g) * 2 - 1) if bkm else (torch.rand(K, N, generator=g) * 2 - 1)).to(dev).bfloat16()
@@ -104,7 +108,7 @@ def gemm_case(lib, case, dev, stream):
     else:
         C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     C2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if epi == 3 else None
-    aux = C if epi == 2 else ((torch.rand(M, N, generator=g) * 4 - 2).to(dev).bfloat16() if epi == 4 else None)
+    aux = C if epi in (2, 7) else ((torch.rand(M, N, generator=g) * 4 - 2).to(dev).bfloat16() if epi == 4 else None)
     ws = torch.empty(max(1, sk * M * N if sk > 1 else 1), device=dev)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
 

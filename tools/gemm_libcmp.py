@@ -16,7 +16,7 @@ from tools.bench_kernels import GEMMS, load  # noqa: E402
 def run(lib, case, dev, stream):
     name, M, N, K, akm, bkm, epi, sk = case
     save_d = epi == 7
-    epi = 3 if save_d else epi
+    epi = 3 if save_d else (7 if epi == 8 else epi)  # 8: EPI_BF16_RESID (7 in the library)
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     A = ((torch.rand(M, K, generator=g) * 2 - 1) if akm else (torch.rand(K, M, generator=g) * 2 - 1)).to(dev).bfloat16()
     B = ((torch.rand(N, K, generator=g) * 2 - 1) if bkm else (torch.rand(K, N, generator=g) * 2 - 1)).to(dev).bfloat16()
@@ -24,7 +24,9 @@ def run(lib, case, dev, stream):
     f32 = epi in (1, 2)
     C = (torch.rand(M, N, generator=g) - 0.5).to(dev) if f32 else torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
     C2 = torch.zeros(M, N, device=dev, dtype=torch.bfloat16) if epi == 3 else None
-    aux = C if epi == 2 else ((torch.rand(M, N, generator=g) * 4 - 2).to(dev).bfloat16() if epi == 4 else None)
+    if epi == 7:
+        C = (torch.rand(M, N, generator=g) * 4 - 2).to(dev).bfloat16()
+    aux = C if epi in (2, 7) else ((torch.rand(M, N, generator=g) * 4 - 2).to(dev).bfloat16() if epi == 4 else None)
     ws = torch.empty(max(1, sk * M * N if sk > 1 else 1), device=dev)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
     rc = lib.vj_gemm_bf16_splitk(M, N, K, p(A), K if akm else M, akm, p(B), K if bkm else N, bkm, epi, p(bias), p(aux),

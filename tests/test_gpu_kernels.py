@@ -870,6 +870,46 @@ def test_gemm_192_row_tiles_match_256(K, pxcd, monkeypatch):
         assert torch.equal(t192["gelu_a"], t192["gelu_nosave"])
 
 
+@pytest.mark.parametrize("K", [32, 96, 384])
+def test_gemm_2w_192x128_tiles_match_256x128(K, monkeypatch):
+    """The two-workgroup kernel on 192 x 128 tiles 64 deep (VJ_GEMM_2W192=1: whole 128-B rows per
+    DMA piece) against its 256 x 128, 32-deep form on the 128-wide shapes it serves (N = 384 / 640):
+    each output's k-steps run in the same order, so every epilogue is BITWISE equal. K = 32 / 96 end
+    in a half-empty 64-deep K-tile (zero-filled), M = 2100 / 1333 in ragged row tiles."""
+    from vjepa2_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(K + 2)
+    for M, N in [(2100, 384), (1333, 640)]:
+        X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+        W = (0.1 * torch.randn(N, K, generator=g)).to(DEV).bfloat16()
+        b = torch.randn(N, generator=g).to(DEV)
+        resid = torch.randn(M, N, generator=g).to(DEV)
+        dgs = torch.randn(M, N, generator=g).to(DEV).bfloat16()
+
+        def run():
+            outs = {"bf16": ops.linear_fwd(X, W, b, ops.EPI_BF16),
+                    "f32": ops.linear_fwd(X, W, b, ops.EPI_F32),
+                    "f32_resid": ops.linear_fwd(X, W, b, ops.EPI_F32_RESID, resid=resid),
+                    "bf16_resid": ops.linear_fwd(X, W, b, ops.EPI_BF16_RESID, resid=resid.bfloat16())}
+            d, a = ops.linear_fwd(X, W, b, ops.EPI_GELU, out=torch.empty(M, N, device=DEV, dtype=torch.bfloat16))
+            outs["gelu_d"], outs["gelu_a"] = d, a
+            gb = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            ops.gemm(M, N, K, X, K, True, W, K, True, ops.EPI_GELU_BWD, out=gb, ldc=N, aux=dgs, ldaux=N)
+            outs["gelu_bwd"] = gb
+            torch.cuda.synchronize()
+            return {k: v.detach().clone() for k, v in outs.items()}
+
+        monkeypatch.setenv("VJ_GEMM_2W192", "1")
+        t192 = run()
+        monkeypatch.setenv("VJ_GEMM_2W192", "0")
+        t256 = run()
+        monkeypatch.delenv("VJ_GEMM_2W192")
+        for k in t192:
+            assert torch.equal(t192[k], t256[k]), f"2W 192x128 != 256x128: {k} M={M} N={N} K={K}"
+        ref = X.float() @ W.float().t() + b
+        _close(t192["f32"], ref, 1e-4 * math.sqrt(K) * 4, 1e-4, "2W 192x128 EPI_F32")
+
+
 def test_transpose_bf16_single_and_batched():
     """Register-tile transpose (8 x 8 blocks per lane, one 64 x 64 tile per wave) and its batched
     form (one launch over a descriptor table, as refresh_weight_transposes uses): bitwise x.t(), on

@@ -60,6 +60,9 @@ __device__ long vj_gemm_stamps[2048 * 16 * 4];
 #ifndef VJ_STG_CPOL
 #define VJ_STG_CPOL 0
 #endif
+#ifndef VJ_DIAG_NODMA
+#define VJ_DIAG_NODMA 0
+#endif
 template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, bool STG = false>
 __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   static_assert(!STG || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256 && EPI != EPI_PARTIAL),
@@ -68,7 +71,9 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   static_assert(NWV == 8 || (NWV == 4 && AK && BKM && !F8), "2-workgroup GEMM: K-major bf16 operands only");
   constexpr int BM = BMT;
   constexpr int MH = BM / 64;     // virtual 16-row m-tiles per half of the wave's rows (4 / 3)
-  constexpr int BK = NWV == 8 ? 64 : 32;
+  // 2-workgroup kernels: 256 x 128 tiles 32 deep (64-B LDS rows), or 192 x 128 tiles 64 deep (128-B
+  // rows: whole cache lines per DMA piece, half the L1 -> L2 requests; 80 KB, no table: RoPE excluded)
+  constexpr int BK = (NWV == 8 || BMT == 192) ? 64 : 32;
   constexpr int NT = NWV * 64;
   constexpr int WNX = NWV / 2;  // waves across N (4 / 2)
   constexpr int WMX = NWV / WNX;          // waves across M (2 / 4)
@@ -88,7 +93,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // K-major B with 4 n blocks per wave: permuted B staging + stores straight from registers (16-B
   // f32 / 8-B bf16 per row); 128-wide tiles would store 4-8 B per lane, so they keep the LDS path
   constexpr bool DIRECT = BKM && NTN == 4;
-  static_assert(BMT == 256 || (BMT == 192 && NWV == 8 && !F8 && AK && DIRECT), "192-row tiles: 8-wave direct K-major bf16");
+  static_assert(BMT == 256 || (BMT == 192 && !F8 && AK && DIRECT && (NWV == 8 || EPI != EPI_ROPE)),
+                "192-row tiles: direct K-major bf16 (the 4-wave kernel without the RoPE table)");
   constexpr bool AUX = EPI == EPI_F32_RESID || EPI == EPI_GELU_BWD || EPI == EPI_BF16_RESID;
   constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_F32_RESID || EPI == EPI_PARTIAL;
 
@@ -105,7 +111,8 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   constexpr int NSL = STG ? ((EPI == EPI_ROPE || GTAB) ? 4 : 5) : 1;
   constexpr int DIST = NSL - 2;
   constexpr int RING0 = GTAB ? 32768 : 0;  // LDS offset of the STG ring
-  __shared__ __attribute__((aligned(16))) char smem_raw[GTAB ? RING0 + 4 * 32768 : STG && NSL == 5 ? 5 * 32768 : 2 * STAGE + TAB_BYTES];
+  constexpr int TABB = (NWV == 4 && BMT == 192) ? 0 : TAB_BYTES;  // 2 x 80 KB per CU leaves no table room
+  __shared__ __attribute__((aligned(16))) char smem_raw[GTAB ? RING0 + 4 * 32768 : STG && NSL == 5 ? 5 * 32768 : 2 * STAGE + TABB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
   LDS_AS char* tab = smem + 2 * STAGE;
   [[maybe_unused]] LDS_AS char* ring = smem + RING0;
@@ -168,6 +175,9 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   auto load_k = [&](__amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, const Tile& T, int t, int slot,
                     int lane) {
     LDS_AS char* s = smem + slot * STAGE;
+#if VJ_DIAG_NODMA
+    if (t >= 2) return;
+#endif
     if (iss) {
       stage<AK, BM, false, DMAW, BK, WNX, PB>(ra, g.lda, g.M - T.m0, t * BK, T.Keff, s, wave, lane);
       stage<BKM, BN, DIRECT, DMAW, BK, WNX, PB>(rb, g.ldb, g.N - T.n0, t * BK, T.Keff, s + A_BYTES, wave, lane);
@@ -581,7 +591,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (!TAIL) {
           if constexpr (SPREAD) {
-            if (iss)
+            if (iss && !VJ_DIAG_NODMA)
               stage<AK, BM, false, DMAW, BK, WNX, PB>(ra, g.lda, g.M - cur.m0, (t + 2) * BK, cur.Keff,
                                                        smem + sl * STAGE, wave, lane);
           } else {
@@ -601,7 +611,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           }
         }
         auto b_pieces = [&] {
-          if (iss)
+          if (iss && !VJ_DIAG_NODMA)
             stage<BKM, BN, DIRECT, DMAW, BK, WNX, PB>(rb, g.ldb, g.N - cur.n0, (t + 2) * BK, cur.Keff,
                                                        smem + sl * STAGE + A_BYTES, wave, lane);
         };
@@ -1114,6 +1124,34 @@ int launch2w(int epi, G256 g, hipStream_t st) {
   return VJ_OK;
 }
 
+// The 4-wave two-workgroup kernel on 192 x 128 tiles, 64 deep: each 1-KB DMA piece is 8 whole 128-B
+// rows, where the 256 x 128 tiles' 32-deep pieces fetch 16 half lines (twice the L1 -> L2 requests,
+// which bound that kernel: profiles/r05_gemm_dma_diag.txt). Bitwise the same outputs; predictor fc2
+// 132 -> 115 us, QKV / proj data gradients -8..-11 %, step +0.4 % (profiles/r05_gemm_2w192_ab.txt).
+// VJ_GEMM_2W192=0 restores the 256 x 128 form; RoPE keeps it (no room for its table at 2 x 80 KB).
+int launch2w192(int epi, G256 g, hipStream_t st) {
+  g.tiles_m = vj_cdiv(g.M, 192);
+  g.group = tile_group(g.tiles_m, g.tiles_n);
+  const dim3 grid(grid256((long)g.tiles_m * g.tiles_n, 2));
+#define L2W(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 128, false, 4, 192>), grid, dim3(256), 0, st, g); break
+  switch (epi) {
+    case EPI_BF16: L2W(EPI_BF16);
+    case EPI_F32: L2W(EPI_F32);
+    case EPI_F32_RESID: L2W(EPI_F32_RESID);
+    case EPI_GELU: L2W(EPI_GELU);
+    case EPI_GELU_BWD: L2W(EPI_GELU_BWD);
+    case EPI_BF16_RESID: L2W(EPI_BF16_RESID);
+    default: vj_set_error("gemm2w192: bad epilogue %d", epi); return VJ_ERR_ARG;
+  }
+#undef L2W
+  VJ_LAUNCH_CHECK("vj_gemm256(2w192)");
+  return VJ_OK;
+}
+bool use_2w192(int epi) {
+  const char* e = getenv("VJ_GEMM_2W192");
+  return !(e && e[0] == '0') && epi != EPI_ROPE;
+}
+
 // one-tile launch; 192-row tiles (BMT = 192) for the K-major 256-wide shapes use_bm192() picks
 int launch192(int epi, const G256& g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
@@ -1237,6 +1275,7 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
   }
   if (a_kmajor && b_kmajor && use_2w(bn == 128)) {
     g.tiles_n = vj_cdiv(N, 128);
+    if (use_2w192(epi)) return launch2w192(epi, g, st);
     return launch2w(epi, g, st);
   }
   if (bn == 256) {

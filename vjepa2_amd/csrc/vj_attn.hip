@@ -192,6 +192,9 @@ __device__ __forceinline__ void stage_rows(__amdgpu_buffer_rsrc_t rs, long ld, i
   constexpr int RB = HDP * 2;                  // bytes per LDS row
   constexpr int PIECES = ROWS * RB / 1024;
   static_assert(ROWS * RB % 1024 == 0, "tile must be whole 1-KB pieces");
+#if VJ_DIAG_NODMA
+  if (row0 >= 2 * ROWS) return;  // timing-only build (wrong results): tiles past the second not loaded
+#endif
   // nwaves is 4 at every call site: pieces wave, wave + 4, ... (fully unrolled, wave is uniform)
 #pragma unroll
   for (int i = 0; i < (PIECES + 3) / 4; ++i) {

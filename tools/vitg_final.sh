@@ -7,6 +7,9 @@ cd "$(dirname "$0")/.." || exit 2
 export TMPDIR=/tmp
 tag=${1:-vitg}
 out=gpurun_out/$tag; mkdir -p "$out"
+# traffic entries go to a copy under gpurun_out (merged back by gpurun; profiles/ on the box is not):
+# copy $out/traffic.json to profiles/traffic.json afterwards
+cp profiles/traffic.json "$out/traffic.json"
 run() {  # name workload bench-args...
   local name=$1 wl=$2; shift 2
   timeout -k 10 400 python -u bench.py --steps 3 --warmup 2 --cpu-baseline 0 "$@" > "$out/$name.log" 2>&1 || { echo "$name failed"; tail -3 "$out/$name.log"; return 3; }
@@ -18,7 +21,8 @@ run() {  # name workload bench-args...
     i=$((i + 1))
     VJ_TGT_STREAM=0 VJ_WGRAD_STREAM=0 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $p -d "$out/${name}_p$i" -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --cpu-baseline 0 --kernel-events 0 --synced-steps 0 "$@" > "$out/${name}_p$i.log" 2>&1 || { echo "$name pmc $p failed"; tail -3 "$out/${name}_p$i.log"; return 4; }
   done
-  python3 tools/traffic.py "$out/${name}_p1" "$out/${name}_p2" "$dom" profiles/traffic.json "$wl" || return 5
+  python3 tools/traffic.py "$out/${name}_p1" "$out/${name}_p2" "$dom" "$out/traffic.json" "$wl" || return 5
+  cp "$out/traffic.json" profiles/traffic.json  # the final line below reads it
   timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --cpu-baseline 0 "$@" > "$out/${name}_final.log" 2>&1 || { echo "$name final failed"; return 3; }
   grep '^{' "$out/${name}_final.log" | tail -1 > "$out/${name}.json"
   cut -c1-600 "$out/${name}.json"

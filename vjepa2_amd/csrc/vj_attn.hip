@@ -32,7 +32,13 @@
 // removed: a K / V^T fragment ring at 4 forward workgroups per CU (spills), the V-tile DMA under the
 // softmax, priority around the backward MFMAs, the fused backward (dQ partials from the dK/dV sweep
 // plus a reduce pass; 192.7 vs 196.9 clips/s) and a separate delta kernel.
-constexpr int KW32 = 2, QW32 = 2, KW64 = 1, QW64 = 1;
+#ifndef VJ_KW32
+#define VJ_KW32 2
+#endif
+#ifndef VJ_QW32
+#define VJ_QW32 2
+#endif
+constexpr int KW32 = VJ_KW32, QW32 = VJ_QW32, KW64 = 1, QW64 = 1;
 // Forward occupancy hint (hd <= 64): the launch bound asks for 2 waves per SIMD, but the kernel compiles
 // to 160 VGPRs (hd 64) / 94 (hd 32) and runs 3 / 5 per SIMD; with the bound at 3 the register allocator
 // lands on 166 and a different schedule: target forward 425.7 -> 415.7 us, N = 8192 725 -> 717 us

@@ -122,6 +122,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, ui
   return __builtin_amdgcn_make_buffer_rsrc((void*)(lo | (hi << 32)), (short)0, n, 0x00020000);
 }
 // 16 bytes per lane, global(rsrc + voffset) -> LDS(lds_wave_base + lane*16). Out-of-range -> zeros.
+// Timing-only diagnostic macros (VJ_DIAG_*: loads skipped or misplaced, WRONG results) exist for
+// variant libraries only (python -m vjepa2_amd.build --variant NAME -DVJ_DIAG_...), never libvjepa_hip.so.
+#if !defined(VJ_VARIANT_BUILD) && (defined(VJ_DIAG_NODMA) || defined(VJ_DIAG_NOWAIT) || defined(VJ_DIAG_SAMEADDR) || \
+                                   defined(VJ_DIAG_FULL128))
+#error "VJ_DIAG_* macros are for variant builds only"
+#endif
 #ifndef VJ_DMA_CPOL
 #define VJ_DMA_CPOL 0
 #endif

@@ -108,7 +108,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // (GTAB: the GELU epilogue by table, 4 slots behind the 28.7-KB table at LDS offset 0, whose byte
   // offsets then fit the 16-bit lanes the lookup computes them in)
   constexpr bool GTAB = STG && EPI == EPI_GELU;
-  constexpr int NSL = STG ? ((EPI == EPI_ROPE || GTAB) ? 4 : 5) : 1;
+#ifndef VJ_STG_NSL4
+#define VJ_STG_NSL4 0  // variant builds: every staggered kernel on 4 ring slots (distance 2)
+#endif
+  constexpr int NSL = STG ? ((EPI == EPI_ROPE || GTAB || VJ_STG_NSL4) ? 4 : 5) : 1;
   constexpr int DIST = NSL - 2;
   constexpr int RING0 = GTAB ? 32768 : 0;  // LDS offset of the STG ring
   constexpr int TABB = (NWV == 4 && BMT == 192) ? 0 : TAB_BYTES;  // 2 x 80 KB per CU leaves no table room

@@ -48,8 +48,9 @@ __device__ long vj_gemm_stamps[2048 * 16 * 4];
 
 
 // NWV = 8: 8 waves (2 x 4), 64-deep K tiles, one workgroup per CU. NWV = 4 ("2W"): 4 waves (2 x 2),
-// 32-deep K tiles, 64 KB of LDS, TWO workgroups per CU, so one workgroup's epilogue (HBM / VALU)
-// runs under the other's main loop (MFMA); K-major operands only.
+// TWO workgroups per CU, so one workgroup's epilogue (HBM / VALU) runs under the other's main loop
+// (MFMA); K-major operands only; 192 x 128 tiles 64 deep (80 KB, the default) or 256 x 128 tiles 32
+// deep (64 KB + the RoPE table area).
 // BMT = 192 (8-wave, K-major bf16, 256-wide direct-store tiles only): 96-row wave tiles (3 m-tiles
 // per M-half) for problems whose 256-row tile count leaves a round of CUs under-filled (context
 // GEMMs, M ~ 11.7k: 184 tiles of 256 x 256 on 256 CUs -> 244 tiles of 192 x 256).

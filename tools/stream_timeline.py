@@ -1,14 +1,20 @@
 """Per-stream timeline of one steady-state train step from a rocprofv3 kernel trace taken with the side
 streams ON (the bench's real configuration): for each phase of the step (forward up to the loss,
 backward + update after it) the busy time of every queue, the time with 0 / 1 / 2+ kernels in flight,
-and the longest single-queue stretches (where one stream alone holds the chip).
+and the kernels that run with nothing else in flight (where one stream alone holds the chip).
 
     python tools/stream_timeline.py <run_kernel_trace.csv> [out.txt]
 """
 import csv
+import re
 import sys
 
 STEP_MARK = "k_jepa_loss"
+
+
+def _short(name):
+    name = re.sub(r"^void\s+", "", name)
+    return re.sub(r"\(anonymous namespace\)::", "", name).split("(")[0][:70]
 
 
 def main(path, out=None):
@@ -46,6 +52,24 @@ def main(path, out=None):
                      f"2+ kernels {hist[2] / 1e6:.2f} ms")
         for q, t in sorted(per_q.items(), key=lambda x: -x[1]):
             lines.append(f"   queue {q}: kernels busy {t / 1e6:.2f} ms")
+    # kernels that run with nothing else in flight (the step's exposed critical path), whole cycle
+    ev = []
+    for i, (s, e, q, n) in enumerate(ks):
+        ev += [(s, 1, i), (e, -1, i)]
+    ev.sort()
+    active, last, alone = set(), t0, {}
+    for t, d, i in ev:
+        if len(active) == 1:
+            k = _short(ks[next(iter(active))][3])
+            alone[k] = alone.get(k, 0) + (t - last)
+        last = t
+        if d == 1:
+            active.add(i)
+        else:
+            active.discard(i)
+    lines.append(f"kernels alone in flight: {sum(alone.values()) / 1e6:.2f} ms; largest:")
+    for k, v in sorted(alone.items(), key=lambda x: -x[1])[:12]:
+        lines.append(f"   {v / 1e6:6.2f} ms  {k}")
     txt = "\n".join(lines)
     print(txt)
     if out:

@@ -350,6 +350,8 @@ def spawn_ranks(n):
     import socket
     import subprocess
 
+    from vjepa2_amd import rank_env
+
     backend = os.environ.get("VJ_DIST_BACKEND", "nccl")
     ndev = torch.cuda.device_count()
     if backend == "nccl" and ndev < n:
@@ -362,8 +364,8 @@ def spawn_ranks(n):
     s.close()
     procs = []
     for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env = rank_env(dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                            MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     code = 0
     alive = list(procs)

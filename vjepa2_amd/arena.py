@@ -209,9 +209,6 @@ class FusedAdamW:
         work = []  # per arena: (arena index, active mask, fuse, target arena)
         for i, (g, a) in enumerate(zip(self.param_groups, self.arenas)):
             act = np.array([id(p) not in ex for p in a.params], dtype=bool)
-            st = self.pstep[i]
-            st[act] += 1
-            advanced.append((i, np.nonzero(act)[0]))
             tgt = ema[0][i] if ema is not None else None
             fuse = tgt is not None and bool(act.all()) and tgt.numel == a.numel
             if tgt is not None and not fuse:
@@ -219,9 +216,13 @@ class FusedAdamW:
             work.append((i, act, fuse, tgt))
         if stages is not None and late_ema:
             # the per-stage events would be recorded before these arenas' EMA writes, so a reader
-            # waiting on them (the next target forward) would race with it
+            # waiting on them (the next target forward) would race with it. Checked before any step
+            # count advances, so a caller may catch this and retry without stages.
             raise ValueError("stages: every EMA'd arena must take the fused AdamW + EMA pass (no excluded "
                              "parameters, equal layout)")
+        for i, act, _, _ in work:
+            self.pstep[i][act] += 1
+            advanced.append((i, np.nonzero(act)[0]))
 
         def run(i, act, fuse, tgt, j, n):
             # maximal runs of active params with equal step count in params [j, n) of arena i

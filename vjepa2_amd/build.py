@@ -48,7 +48,8 @@ def build(verbose=True, force=False, variant=None, defines=()):
     lib = os.path.join(HERE, f"libvjepa_hip_{variant}.so") if variant else LIB
     flags = CFLAGS + [f"-D{d}" for d in defines]
     if variant:
-        flags.append("-DVJ_VARIANT_BUILD=1")  # unlocks the timing-only VJ_DIAG_* macros (vj_common.h)  # experiments: extra compiler flags for every source (e.g. VJ_EXTRA_FLAGS=-fno-slp-vectorize)
+        flags.append("-DVJ_VARIANT_BUILD=1")  # unlocks the timing-only VJ_DIAG_* macros (vj_common.h)
+        # experiments: extra compiler flags for every source (e.g. VJ_EXTRA_FLAGS=-fno-slp-vectorize)
         flags += os.environ.get("VJ_EXTRA_FLAGS", "").split()
     os.makedirs(objdir, exist_ok=True)
     jobs = []

@@ -86,10 +86,16 @@ class GradReducer:
         for i, b in enumerate(self.buckets):
             for p in b.params:
                 self.owner[id(p)] = i
+        from . import functions
+
+        self._after_join = functions.join_queue()  # this reducer's collectives awaiting a stream join
         self.reset()
 
     def reset(self):
         self.armed = True  # False during the backward of all but the last frames-per-clip group
+        # a backward that raised after queueing buckets must not leave them to fire in the next step
+        # (one rank's extra collective would desync the collective order across ranks)
+        self._after_join.clear()
         for b in self.buckets + self.tail:
             b.pending = {id(p) for p in b.params}
             b.work = None
@@ -101,29 +107,23 @@ class GradReducer:
     def _issue(self, b):
         # With the weight-gradient stream on (functions.wgrad_stream), the bucket's weight gradients
         # may still be in flight there, and its LayerNorm / bias gradients were written on the current
-        # stream. The collective is queued to go out on the weight-gradient stream right after that
-        # stream's next join with the current one (the next block's first weight-gradient launch, a few
-        # launches later), so it sees both without a join of its own: a join per bucket cost 2.8 % of
-        # the step (profiles/r05_reducer_joins_ab.txt). Queue order = bucket order on every rank.
+        # stream. The collective is queued (in this reducer's own queue) to go out on the weight-gradient
+        # stream right after that stream's next join with the current one (the next block's first
+        # weight-gradient launch, a few launches later), so it sees both without a join of its own: a
+        # join per bucket cost 2.8 % of the step (profiles/r05_reducer_joins_ab.txt). Queue order =
+        # bucket order on every rank.
         from . import functions
 
-        side = functions.wgrad_stream()
-        if side is None:
+        if functions.wgrad_stream() is None:
             self._all_reduce(b)
             return
-        functions._AFTER_JOIN.append(lambda b=b: self._all_reduce(b))
+        self._after_join.append(lambda b=b: self._all_reduce(b))
 
     def _flush(self):
-        """Issue the queued collectives now: one join of the weight-gradient stream with the current."""
+        """Issue this reducer's queued collectives now (one join of the weight-gradient stream)."""
         from . import functions
 
-        if not functions._AFTER_JOIN:
-            return
-        side = functions.wgrad_stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            while functions._AFTER_JOIN:
-                functions._AFTER_JOIN.pop(0)()
+        functions.drain_join_queue(self._after_join)
 
     def mark_ready(self, module):
         """Hook called when `module`'s backward has finished writing its parameter gradients."""

@@ -351,11 +351,54 @@ def join_wgrad_stream():
 
 
 _WG_JOIN_TASK = [None]  # autograd graph task whose end-of-backward join is queued
-# Work to issue on the weight-gradient stream right after its next join with the current stream
-# (distributed.GradReducer: a bucket's all-reduce also needs the LayerNorm / bias gradients written on
-# the current stream; riding on the join every block's weight gradients take anyway saves a join of
-# its own per bucket).
-_AFTER_JOIN = []
+
+
+class JoinQueue(list):
+    """Work to issue on the weight-gradient stream right after its next join with the current stream
+    (distributed.GradReducer: a bucket's all-reduce also needs the LayerNorm / bias gradients written on
+    the current stream; riding on the join every block's weight gradients take anyway saves a join of
+    its own per bucket). One queue per owner, so two armed reducers in one process (a trainer and an
+    eval probe, two frames-per-clip groups) never issue each other's collectives; at a join the queues
+    are drained in the order their owners were created, which is the same host program order on every
+    rank, whatever the interleaving of the owners' backward hooks."""
+
+
+_JOIN_QUEUES = []  # weakrefs to the live JoinQueues, creation order
+
+
+def join_queue():
+    q = JoinQueue()
+    _JOIN_QUEUES.append(weakref.ref(q))
+    return q
+
+
+def _drain_join_queues():
+    """Issue every queued item (called on the weight-gradient stream, right after a join)."""
+    live = []
+    for r in _JOIN_QUEUES:
+        q = r()
+        if q is None:
+            continue
+        live.append(r)
+        while q:
+            q.pop(0)()
+    _JOIN_QUEUES[:] = live
+
+
+def drain_join_queue(q):
+    """Issue q's items now: after one join of the weight-gradient stream with the current stream, on
+    it; directly when that stream is off (VJ_WGRAD_STREAM=0 set since the items were queued)."""
+    if not q:
+        return
+    side = wgrad_stream()
+    if side is None:
+        while q:
+            q.pop(0)()
+        return
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        while q:
+            q.pop(0)()
 
 
 def _join_at_backward_end():
@@ -386,8 +429,7 @@ class _OnWgradStream:
             _WG_JOIN_TASK[0] = task
         self.ctx = torch.cuda.stream(self.side)
         self.ctx.__enter__()
-        while _AFTER_JOIN:
-            _AFTER_JOIN.pop(0)()
+        _drain_join_queues()
         return self
 
     def __exit__(self, *exc):

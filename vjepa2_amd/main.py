@@ -132,6 +132,9 @@ def launch(fname, devices):
     check_devices(devices, os.environ.get("VJ_DIST_BACKEND", "nccl"))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    from . import rank_env
+
+    rank_env(os.environ)  # the spawned ranks inherit it: 8 hardware queues before their first HIP call
     ctx = mp.get_context("spawn")
     procs = [ctx.Process(target=process_main, args=(r, fname, world, devices), name=f"rank{r}") for r in range(world)]
     for p in procs:

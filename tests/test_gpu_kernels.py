@@ -730,21 +730,27 @@ def test_gemm_256_tiles_vs_fp32(K, pxcd, monkeypatch):
         _close(a, torch.nn.functional.gelu(pre), 2e-3, 1.5e-2, "EPI_GELU vs gelu(bf16 pre-activation)")
 
 
-@pytest.mark.parametrize("K", [32, 64, 96, 384, 1024])
+@pytest.mark.parametrize("K", [32, 64, 96, 128, 192, 384, 1024])
 @pytest.mark.parametrize("pxcd", [None, "1", "3"])
-def test_gemm_staggered_matches_one_tile(K, pxcd, monkeypatch):
-    """The staggered main loop (VJ_GEMM_STG=1: 32-deep K units in a 4-slot LDS ring, one stream of
-    units across the block's tiles, waves 4-7 one barrier behind waves 0-3) runs the same MFMAs on
-    every accumulator in the same K order as the one-tile kernel, so every epilogue's output is
-    bitwise equal. K = 32 / 64 / 96 make 1 / 2 / 3 units per tile (the DMA stream runs 2 units ahead,
-    i.e. up to 2 tiles ahead), VJ_GEMM_PXCD = 1 / 3 give many tiles per block (epilogue / tile
-    hand-over paths of both wave halves), M = 2100 / 1333 ragged last row tiles, N = 1000 a ragged
-    last column tile; plus the fused QKV + RoPE epilogue."""
+@pytest.mark.parametrize("form", ["1", "2"])
+def test_gemm_staggered_matches_one_tile(K, pxcd, form, monkeypatch):
+    """The staggered main loops (VJ_GEMM_STG=1) run the same MFMAs on every accumulator in the same K
+    order as the one-tile kernel, so every epilogue's output is bitwise equal. Form 1 (VJ_GEMM_STG64=0):
+    32-deep K units in a 4/5-slot LDS ring, one stream of units across the block's tiles, waves 4-7 one
+    barrier behind waves 0-3; K = 32 / 64 / 96 make 1 / 2 / 3 units per tile (the DMA stream runs 2-3
+    units, i.e. up to 3 tiles, ahead). Form 2 (S64, VJ_GEMM_STG64=1, K % 64 == 0; form 1 otherwise):
+    64-deep steps of 128-row granules, A and B streamed by the two wave halves 3 granules ahead; K = 64 /
+    128 / 192 make 1 / 2 / 3 steps per tile (the streams run up to 3 tiles ahead, where a wave half's
+    stream crosses tiles at a different point than the other's). VJ_GEMM_PXCD = 1 / 3 give many tiles
+    per block (epilogue / tile hand-over paths of both wave halves), M = 2100 / 1333 ragged last row
+    tiles (S64: a tile whose A1 granule is empty), N = 1000 a ragged last column tile; plus the fused
+    QKV + RoPE epilogue."""
     from vjepa2_amd import ops
 
     if pxcd:
         monkeypatch.setenv("VJ_GEMM_PXCD", pxcd)
     monkeypatch.setenv("VJ_GEMM_BM192", "0")  # 256-row tiles for both
+    monkeypatch.setenv("VJ_GEMM_STG64", "1" if form == "2" else "0")
     g = torch.Generator(device="cpu").manual_seed(K + 7)
     for M, N in [(2100, 512), (1333, 1000)]:
         X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
@@ -788,7 +794,7 @@ def test_gemm_staggered_matches_one_tile(K, pxcd, monkeypatch):
     assert torch.equal(res[0], res[1]), f"staggered qkv_rope != one-tile kernel (K={K} pxcd={pxcd})"
 
 
-@pytest.mark.parametrize("stg", ["1", "0"])
+@pytest.mark.parametrize("stg", ["1", "0", "2"])
 def test_gelu_epilogues_bitwise_all_bf16(stg, monkeypatch):
     """The fc1 GEMM's GELU epilogues against the exact evaluation (vj_gelu_eval: gelu_fwd_grad on the
     bf16 input) on EVERY bf16 pre-activation: X = 0 and the bias holds the 65536 bf16 values, so
@@ -797,7 +803,8 @@ def test_gelu_epilogues_bitwise_all_bf16(stg, monkeypatch):
     evaluation. Bitwise on every non-NaN input (the -0 pattern enters as +0: 0 + -0 = +0), NaN -> NaN."""
     from vjepa2_amd import ops
 
-    monkeypatch.setenv("VJ_GEMM_STG", stg)
+    monkeypatch.setenv("VJ_GEMM_STG", "1" if stg == "2" else stg)  # "2": the S64 form (K = 64)
+    monkeypatch.setenv("VJ_GEMM_STG64", "1" if stg == "2" else "0")
     monkeypatch.setenv("VJ_GEMM_BM192", "0")
     n = 65536
     bits = torch.arange(n, dtype=torch.int32)
@@ -807,7 +814,7 @@ def test_gelu_epilogues_bitwise_all_bf16(stg, monkeypatch):
     pre = bits.clone()
     pre[pre == -32768] = 0  # 0 + (-0) = +0
     y_ref, dy_ref = ops.gelu_eval(pre.view(torch.bfloat16).to(DEV).contiguous())
-    M, K = 1024, 32
+    M, K = 1024, (64 if stg == "2" else 32)
     X = torch.zeros(M, K, device=DEV, dtype=torch.bfloat16)
     W = torch.zeros(n, K, device=DEV, dtype=torch.bfloat16)
     d, a = ops.linear_fwd(X, W, bias, ops.EPI_GELU, out=torch.empty(M, n, device=DEV, dtype=torch.bfloat16))

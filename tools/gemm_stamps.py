@@ -11,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import bench_kernels as bk  # noqa: E402
 
-lib = bk.load(os.path.join(bk.HERE, "vjepa2_amd", "libvjepa_hip_stamps.so"))
+lib = bk.load(os.environ.get("VJ_STAMPS_LIB") or os.path.join(bk.HERE, "vjepa2_amd", "libvjepa_hip_stamps.so"))
 dev = torch.device("cuda")
 stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 only = sys.argv[1] if len(sys.argv) > 1 else "tgt"
@@ -33,6 +33,13 @@ for case in bk.GEMMS:
     t0 = st[:, :, 0][valid].min()
     end = st[:, :, 2][valid].max()
     ntile = valid.sum(1)
+    k1 = st[:, :, 3][valid]
+    if (k1 != 0).all():  # staggered builds: first 64-deep K step vs the rest of the main loop
+        nks = case[3] // 64
+        first = (k1 - st[:, :, 0][valid])
+        rest = (st[:, :, 1][valid] - k1) / max(1, nks - 1)
+        print(f"{case[0]:22s} first K step {np.median(first):8.0f} cyc (p90 {np.percentile(first, 90):.0f})  "
+              f"later steps {np.median(rest):7.0f} cyc each", flush=True)
     print(f"{case[0]:22s} tiles/block {ntile[ntile > 0].min()}-{ntile.max()}  main {np.median(main):8.0f} cyc  "
           f"epi {np.median(epi):8.0f} cyc (p10 {np.percentile(epi, 10):.0f} p90 {np.percentile(epi, 90):.0f})  "
           f"span {end - t0} cyc", flush=True)

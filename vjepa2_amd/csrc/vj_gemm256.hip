@@ -20,6 +20,7 @@
 // Epilogue: stores straight from registers (K-major B, 256-wide tiles: B rows staged permuted) or
 // through a padded LDS image in the freed slot, with bias / residual / GELU / GELU' / RoPE fused.
 #include <stdlib.h>
+#include <atomic>
 #include <type_traits>
 #include "vj_gemm_tile.h"
 
@@ -46,6 +47,17 @@ namespace {
 __device__ long vj_gemm_stamps[2048 * 16 * 4];
 #endif
 
+// counted wait for this wave's vector-memory operations (LDS-DMA pieces included): at most N in flight
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N == 0 || N == 4 || N == 8 || N == 12 || N == 16, "vm_wait: add the count");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
+
 
 // NWV = 8: 8 waves (2 x 4), 64-deep K tiles, one workgroup per CU. NWV = 4 ("2W"): 4 waves (2 x 2),
 // TWO workgroups per CU, so one workgroup's epilogue (HBM / VALU) runs under the other's main loop
@@ -64,7 +76,7 @@ __device__ long vj_gemm_stamps[2048 * 16 * 4];
 #ifndef VJ_DIAG_NODMA
 #define VJ_DIAG_NODMA 0
 #endif
-template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, bool STG = false>
+template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, int STG = 0>
 __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   static_assert(!STG || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256 && EPI != EPI_PARTIAL),
                 "staggered main loop: 8-wave K-major bf16 256 x 256 tiles");
@@ -114,6 +126,32 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
 #endif
   constexpr int NSL = STG ? ((EPI == EPI_ROPE || GTAB || VJ_STG_NSL4) ? 4 : 5) : 1;
   constexpr int DIST = NSL - 2;
+  // S64 (STG == 2, round 6): the staggered loop on 64-deep K steps, so every 1-KB LDS-DMA piece is 8
+  // WHOLE 128-B rows (the 32-deep units above fetch 16 half lines: twice the L1 -> L2 requests, which
+  // bound that loop - profiles/r05_gemm_dma_diag.txt). The LDS budget is kept by splitting each K step
+  // of the tile into 16-KB granules of 128 rows x 64: A0 / A1 (tile rows 0-127 / 128-255) and Blo / Bhi
+  // (columns 0-127 / 128-255). Waves 0-3 stream the A granules, waves 4-7 the B granules, one granule
+  // per wave group and load interval (4 pieces per wave). A wave (wr, wc) owns rows {128 h + 64 wr +
+  // 0..63 : h = 0, 1} x columns 64 wc + 0..63; per K step it runs L0 (A0 and B fragments: 16
+  // ds_read_b128) | M0 (rows of A0: 32 MFMAs) | L1 (A1 fragments, B kept in registers: 8 reads) | M1,
+  // waves 4-7 one interval behind as before. Every output sums the same MFMAs in the same k order as
+  // the other forms: bitwise the same results. Rings: SA A slots, SB B slots (DMA distance SA - 1 /
+  // SB - 1 granules, 4 + 4 x 16 KB = the 4-slot ring's 128 KB, beside the GELU / RoPE tables).
+  constexpr bool S64 = STG == 2;
+  constexpr int GSZ = 16384;
+  constexpr int SA = 4, SB = 4;
+  constexpr int EA = SA - 1, EB = SB - 1;
+  static_assert(EA >= 2 && EB >= 3, "S64 waits assume at least one interval of DMA lead");
+  // first row of the wave's rows (S64: the wave's 64-row band in each 128-row half) and the first row
+  // of virtual m-tile i relative to it
+  constexpr int WRS = S64 ? 64 : WM;
+  // where the S64 loads issue their DMA pieces (VJ_S64_DMA): 0 = one granule in each load interval;
+  // 1 = both groups' two granules in L1 (L0 holds 16 fragment reads, L1 8); 2 = A's in L1, B's split
+#ifndef VJ_S64_DMA
+#define VJ_S64_DMA 0
+#endif
+  constexpr bool S64_AL1 = VJ_S64_DMA >= 1, S64_BL1 = VJ_S64_DMA == 1;
+  auto rowoff = [](int i) { return S64 ? (i >> 2) * 128 + (i & 3) * 16 : i * 16; };
   constexpr int RING0 = GTAB ? 32768 : 0;  // LDS offset of the STG ring
   constexpr int TABB = (NWV == 4 && BMT == 192) ? 0 : TAB_BYTES;  // 2 x 80 KB per CU leaves no table room
   __shared__ __attribute__((aligned(16))) char smem_raw[GTAB ? RING0 + 4 * 32768 : STG && NSL == 5 ? 5 * 32768 : 2 * STAGE + TABB];
@@ -284,7 +322,55 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       }
     }
   };
-  if constexpr (STG) {
+  // ---- S64 stream: this wave group's operand (A: waves 0-3, B: waves 4-7) as granules; position dq of
+  // the group's stream = (tile, step dk >> 1, half dk & 1), into slot dq % SA (A) / SA + dq % SB (B).
+  // Each wave DMAs rows 32 (wave & 3) .. + 31 of every granule (4 pieces of 8 rows); its lane offsets
+  // are fixed for the launch (rows relative to the granule's first row), the descriptor's range check
+  // (from that row to the operand's end) zero-fills rows past M / N and, past the stream end (dleft 0),
+  // whole granules, so the per-wave vmcnt counts never change.
+  [[maybe_unused]] const int nks = S64 ? g.K >> 6 : 0;
+  [[maybe_unused]] const long dld = isA ? g.lda : g.ldb;
+  [[maybe_unused]] const bf16_t* dbase = isA ? g.A : g.B;
+  [[maybe_unused]] int dleft = 0, dq = 0, dk = 0, q64 = 0;
+  auto dma_setup64 = [&]() {
+    if (dwg < runend) {
+      const Tile T = make_tile(dwg);
+      dbase = isA ? g.A + (long)T.m0 * g.lda : g.B + (long)T.n0 * g.ldb;
+      dleft = isA ? g.M - T.m0 : g.N - T.n0;
+    } else {
+      dleft = 0;
+    }
+  };
+  auto dma_gran = [&]() {
+    const int h = dk & 1;
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(dbase + (h ? 128 * dld : 0), clampb((long)(dleft - 128 * h) * dld * 2));
+    const int soff = __builtin_amdgcn_readfirstlane((dk >> 1) * 128);
+    LDS_AS char* dst = ring + (isA ? dq % SA : SA + dq % SB) * GSZ + (wave & 3) * 4096;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst + k * 1024, 16, dvo[k], soff, 0, VJ_STG_CPOL);
+    ++dq;
+    if (++dk == 2 * nks) {
+      dk = 0;
+      dwg += P;
+      dma_setup64();
+    }
+  };
+  if constexpr (S64) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = 32 * (wave & 3) + 8 * k + (lane >> 3);  // granule row of the lane's 16-B chunk
+      const int c = (lane & 7) ^ ((r >> 1) & 7);            // its logical chunk (128-B row swizzle)
+      const int rl = r & 63;                                 // B: PERM within 64-row groups (stage())
+      const int gr = isA ? r : (r - rl) + 4 * (rl & 15) + (rl >> 4);
+      dvo[k] = (uint32_t)(gr * dld * 2 + c * 16);
+    }
+    dma_setup64();
+#pragma unroll
+    for (int i = 0; i < EA; ++i) dma_gran();
+    static_assert(EA == EB, "the prologue issues EA granules on both streams");
+    if (!isA && S64_BL1) dma_gran();  // B all in L1: two K steps (4 granules) ahead
+  } else if constexpr (STG) {
     dma_setup();
 #pragma unroll
     for (int i = 0; i < DIST; ++i) {
@@ -311,7 +397,6 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   f32x4 acc[2 * MH][NTN];
   auto accv = [&](int i, int j, int r) -> float { return acc[i][j][r]; };
   auto accs = [&](int i, int j, int r, float v) { acc[i][j][r] = v; };
-  auto rowoff = [](int i) { return i * 16; };
   bf16x8 Aa[MH], Ab[MH], Ba[NTN], Bb[NTN];
   // A fragments of M-half mh (4 m-tiles), k-step ks; B fragments of all NTN n-tiles, k-step ks
   auto rdA = [&](bf16x8 (&X)[MH], int slot, int mh, int ks) {
@@ -392,6 +477,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   for (;;) {
 #if VJ_GEMM_STAMPS
     const long st0 = __builtin_amdgcn_s_memtime();
+    long st_k1 = 0;  // staggered loops: after the tile's first 64-deep K step
 #endif
     const int wgn = wg + P;
     const bool has_next = wgn < runend;
@@ -445,7 +531,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     [[maybe_unused]] f32x4 auxr[AUX && STG ? 4 : 1];
     auto stg_aux = [&] {
       if constexpr (AUX && STG) {
-        const int m = cur.m0 + wr * WM + 4 * (lane >> 4);
+        const int m = cur.m0 + wr * WRS + 4 * (lane >> 4);
         const int n = cur.n0 + wc * WN + NTN * (lane & 15);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -460,7 +546,88 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         }
       }
     };
-    if constexpr (STG) {
+    if constexpr (S64) {
+      // S64 main loop (above). Waits, with j = the group's load-interval index (A position j / B
+      // position j are DMA'd EA / EB intervals ahead): waves 0-3 end every L with A position j + 1
+      // landed (vmcnt(4 (EA - 1))); waves 4-7 end each L1 with the next step's Blo / Bhi (B positions
+      // up to j + 2) landed (vmcnt(4 (EB - 2))); the barrier after an L publishes them to every wave.
+      // The aux rows of a residual / saved-derivative epilogue (4 loads per lane) are fetched in the last
+      // step's L0, after its DMA pieces: the L1 waits after them count 4 more.
+      if (wg == run0 + jb) {  // first tile: A position 0 and B positions 0, 1 landed, RoPE table published
+        if (isA || S64_BL1) vm_wait<8>();
+        else vm_wait<4 * (EB - 2)>();
+        __builtin_amdgcn_s_barrier();
+        if (wr == 1) __builtin_amdgcn_s_barrier();
+      }
+      auto bar = [] {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      // Aa / Ab: A fragments (m-tiles 0-3 of the wave's band) at k-steps 0 / 1; Ba / Bb: B fragments
+      auto mm64 = [&](auto h_c) {
+        constexpr int h = decltype(h_c)::value;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[4 * h + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Aa[i], Ba[j], acc[4 * h + i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[4 * h + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ab[i], Bb[j], acc[4 * h + i][j], 0, 0, 0);
+      };
+      const int qt = q64;  // stream position of this tile's A0 / Blo of step 0
+      for (int s = 0; s < nks; ++s) {
+        const int p = qt + 2 * s;
+        const LDS_AS char* sA0 = ring + (p % SA) * GSZ;
+        const LDS_AS char* sA1 = ring + ((p + 1) % SA) * GSZ;
+        const LDS_AS char* sB = ring + (SA + (p + (wc >> 1)) % SB) * GSZ;
+        const bool last = s + 1 == nks;
+        // L0
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Aa[i] = frag<true, 128, 64>(sA0, wr * 64 + i * 16, 0, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Ba[j] = frag<true, 128, 64>(sB, (wc & 1) * 64 + j * 16, 0, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ab[i] = frag<true, 128, 64>(sA0, wr * 64 + i * 16, 1, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Bb[j] = frag<true, 128, 64>(sB, (wc & 1) * 64 + j * 16, 1, lane);
+        if (isA ? !S64_AL1 : !S64_BL1) dma_gran();
+        if (isA) {
+          if constexpr (S64_AL1) vm_wait<4>();  // A1(s) landed; A0(s + 1) in flight
+          else vm_wait<4 * (EA - 1)>();
+        }
+        if (AUX && last) stg_aux();
+        bar();
+        mm64(std::integral_constant<int, 0>{});
+        bar();
+        // L1
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Aa[i] = frag<true, 128, 64>(sA1, wr * 64 + i * 16, 0, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Ab[i] = frag<true, 128, 64>(sA1, wr * 64 + i * 16, 1, lane);
+        dma_gran();
+        if (isA ? S64_AL1 : S64_BL1) dma_gran();
+        // counts: pieces issued after the awaited granule (+ 4 aux loads in the last step)
+        constexpr int WA = S64_AL1 ? 8 : 4 * (EA - 1), WB = S64_BL1 ? 8 : 4 * (EB - 2);
+        if (AUX && last) {
+          if (isA) vm_wait<WA + 4>();
+          else vm_wait<WB + 4>();
+        } else {
+          if (isA) vm_wait<WA>();
+          else vm_wait<WB>();
+        }
+        bar();
+        mm64(std::integral_constant<int, 1>{});
+#if VJ_GEMM_STAMPS
+        if (s == 0) st_k1 = __builtin_amdgcn_s_memtime();
+#endif
+        if (!last || wr == 0) bar();
+      }
+      q64 = qt + 2 * nks;
+    } else if constexpr (STG) {
       // Staggered main loop. Per unit, each wave runs L | M (intervals between workgroup
       // barriers): L = the unit's fragment reads (A m-tiles 0-7, B n-tiles 0-3: 12 ds_read_b128) + its
       // 4 DMA pieces of unit q + 2, M = the unit's 32 MFMAs. Waves 4-7 run one interval behind waves
@@ -515,6 +682,9 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         bar();
         mm(Aa, 0, Ba);
         mm(Ab, 1, Ba);
+#if VJ_GEMM_STAMPS
+        if (u == 1) st_k1 = __builtin_amdgcn_s_memtime();
+#endif
         if (u + 1 < nku || wr == 0) bar();
       }
     } else {
@@ -677,7 +847,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // no LDS round trip.
       const int nb = cur.n0 + wc * WN + NTN * (lane & 15);
       const bool nok = nb < g.N;
-      const int mb = cur.m0 + wr * WM + lrow;
+      const int mb = cur.m0 + wr * WRS + lrow;
       float bias[NTN];
 #pragma unroll
       for (int j = 0; j < NTN; ++j) bias[j] = STG ? biasp[j] : 0.f;
@@ -851,7 +1021,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
 #pragma unroll
           for (int j = 0; j < NTN; ++j) v[j] = accv(i, j, r) + bias[j];
           if constexpr (EPI == EPI_ROPE) {
-            const int rp = rpos[wr * WM + rowoff(i) + lrow + r];
+            const int rp = rpos[wr * WRS + rowoff(i) + lrow + r];
 #pragma unroll
             for (int p = 0; p < NTN / 2; ++p) {
               if (!ract[p]) continue;
@@ -1015,11 +1185,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
 
 #if VJ_GEMM_STAMPS
     {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (!STG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // STG: the DMA stream runs on
       const long st2 = __builtin_amdgcn_s_memtime();
       if (threadIdx.x == 0 && blockIdx.x < 2048 && stamp_it < 16) {
         long* d = vj_gemm_stamps + ((long)blockIdx.x * 16 + stamp_it) * 4;
-        d[0] = st0; d[1] = st1; d[2] = st2; d[3] = __builtin_amdgcn_s_memrealtime();
+        d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st_k1;
       }
       ++stamp_it;
     }
@@ -1052,8 +1222,15 @@ int num_cus() {
 // the same number of blocks. VJ_GEMM_PXCD caps the blocks per XCD (tests: many tiles per block).
 // (A phase offset between the blocks of an XCD, so odd blocks' epilogues fall under the even
 // blocks' main loops, measured no gain in round 3 and was removed.)
+// CUs the persistent grids leave free (vj_set_reserved_cus): while a data-parallel rank's gradient
+// buckets are all-reduced, RCCL's channel kernels hold CUs; a persistent GEMM block that cannot be
+// placed on one of them only starts when it frees, and its statically assigned tiles then run after
+// every other block's (measured on one GPU with a 16-CU proxy copy: step -11.6 %,
+// profiles/r06_rccl_proxy_ab.txt). Set by distributed.GradReducer around its bucket window.
+std::atomic<int> g_reserved_cus{0};
+
 int grid256(long nb, int per_cu = 1) {
-  int per_xcd = per_cu * num_cus() / 8;
+  int per_xcd = per_cu * (num_cus() - g_reserved_cus.load(std::memory_order_relaxed)) / 8;
   const char* e = getenv("VJ_GEMM_PXCD");
   if (e && atoi(e) > 0) per_xcd = atoi(e);
   if (per_xcd < 1) per_xcd = 1;
@@ -1191,22 +1368,36 @@ bool use_bm192(int M, int tn) {
   return r192 * 192 * 108 < r256 * 256 * 85;
 }
 
-// Staggered main loop (STG) for the K-major 256 x 256-tile GEMMs with K % 32 == 0. VJ_GEMM_STG: 0 = never,
-// 1 = always (where the shape takes 256-row tiles), unset = the measured default: the epilogues that
-// read no aux rows (GELU, RoPE, bf16 / f32 out). Measured in the train step (rocprofv3, one call,
-// profiles/r04_gemm_staggered_step.txt): GELU -1.8 %, RoPE -1.6 %, bf16 -1.7 %, but the residual /
-// saved-derivative epilogues +1..+4 % (bf16 residual, K = 4096 target fc2: +4 %).
-bool use_stg(int K, int epi) {
-  if (K % 32) return false;
+// Staggered main loop (STG) for the K-major 256 x 256-tile GEMMs: form 1 = 32-deep units (K % 32 == 0),
+// form 2 = S64, 64-deep whole-line granules (K % 64 == 0); 0 = the one-tile kernel. Measured, round 4
+// (profiles/r04_gemm_staggered_step.txt): form 1 pays on the GELU / RoPE / bf16 / f32 epilogues (-1.6..-1.8 %
+// in the step) and not on the residual / saved-derivative ones. Round 6 (profiles/r06_gemm_s64.txt):
+// isolated, S64 runs a K step 3-4 % faster where the operand panels stream from beyond L2 (K = 4096:
+// target fc2 -2.4..-4 %) and takes the residual epilogues below the one-tile kernel (target proj / fc2,
+// bf16 or f32 residual, -1..-4 %), but is 4-12 % slower per K step on the L2-resident K = 1024 panels of
+// the QKV / GELU / RoPE / data-gradient GEMMs; in the train step, where the side streams' GEMMs share the
+// chip (and its L2), S64 on every shape beats both the round-5 choice (+0.8 %) and S64 only on K >= 2048
+// and the residual epilogues (+0.55 %), two interleaved runs each in one call. Default: S64 wherever
+// K % 64 == 0, else form 1 on the epilogues without aux rows. VJ_GEMM_STG: 0 = never, 1 = every epilogue
+// (form 1 where S64 cannot run); VJ_GEMM_STG64: 0 / 1 forces form 1 / 2 wherever a staggered loop runs.
+int use_stg(int K, int epi) {
+  if (K % 32) return 0;
   const char* e = getenv("VJ_GEMM_STG");
-  if (e && e[0] == '0') return false;
-  if (e && e[0] == '1') return true;
-  return epi == EPI_GELU || epi == EPI_ROPE || epi == EPI_BF16 || epi == EPI_F32;
+  if (e && e[0] == '0') return 0;
+  const bool aux = epi == EPI_F32_RESID || epi == EPI_BF16_RESID || epi == EPI_GELU_BWD;
+  int form = 2;
+  const char* f = getenv("VJ_GEMM_STG64");
+  if (f && f[0] == '0') form = 1;
+  if (f && f[0] == '1') form = 2;
+  if (form == 2 && K % 64) form = 1;
+  if (aux && form == 1 && !(e && e[0] == '1')) return 0;
+  return form;
 }
 
+template <int FORM>
 int launch_stg(int epi, const G256& g, hipStream_t st) {
   const dim3 grid(grid256((long)g.tiles_m * g.tiles_n));
-#define LSTG(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 256, true>), grid, dim3(512), 0, st, g); break
+#define LSTG(E) hipLaunchKernelGGL((k_gemm256<true, true, E, 256, false, 8, 256, FORM>), grid, dim3(512), 0, st, g); break
   switch (epi) {
     case EPI_BF16: LSTG(EPI_BF16);
     case EPI_F32: LSTG(EPI_F32);
@@ -1254,6 +1445,12 @@ int launch256(int epi, const G256& g, hipStream_t st) {
 
 }  // namespace
 
+extern "C" int vj_set_reserved_cus(int n) {
+  VJ_CHECK_ARG(n >= 0 && n <= num_cus() - 8, "vj_set_reserved_cus: %d of %d CUs", n, num_cus());
+  g_reserved_cus.store(n, std::memory_order_relaxed);
+  return VJ_OK;
+}
+
 // 256-wide column tiles unless the last one would waste more than 15 % of the work (measured,
 // tools/bench_kernels.py: predictor QKV N = 1152 -17 % with 256-wide tiles; N = 384 +14 %)
 bool wide_tile_ok(int N) { return N % 256 == 0 || (N > 256 && vj_cdiv(N, 256) * 256L * 100 <= 115L * N); }
@@ -1288,7 +1485,11 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
       g.group = tile_group(g.tiles_m, tn);
       return launch192(epi, g, st);
     }
-    if (a_kmajor && b_kmajor && use_stg(K, epi)) return launch_stg(epi, g, st);
+    if (a_kmajor && b_kmajor) {
+      const int form = use_stg(K, epi);
+      if (form == 2) return launch_stg<2>(epi, g, st);
+      if (form == 1) return launch_stg<1>(epi, g, st);
+    }
     if (a_kmajor && b_kmajor) return launch256<true, true, 256>(epi, g, st);
     if (a_kmajor && !b_kmajor) return launch256<true, false, 256>(epi, g, st);
     if (!a_kmajor && b_kmajor) return launch256<false, true, 256>(epi, g, st);

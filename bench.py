@@ -106,6 +106,9 @@ def main():
     ap.add_argument("--arm-reducer", type=int, default=0,
                     help="at --gpus 1: arm the bucketed gradient all-reduce over a one-rank process group "
                          "(VJ_DIST_BACKEND, default nccl = RCCL) to price what N > 1 adds to the step")
+    ap.add_argument("--rccl-proxy-cus", type=int, default=0,
+                    help="with the reducer armed: a copy of 2x every bucket on N persistent workgroups beside its "
+                         "all-reduce, pricing the CUs RCCL's channel kernels hold at world > 1 (diagnostic)")
     args = ap.parse_args()
     if args.gpus > 1 and "RANK" not in os.environ:
         # no launcher: start one rank process per GPU from this GPU-free parent
@@ -155,6 +158,8 @@ def main():
     armed = args.arm_reducer == 1 or world > 1  # --arm-reducer 2: the process group only (diagnostics)
     trainer = JEPATrainer(enc, pred, tgt, opt, mixed_precision=True, loss_exp=1.0, world_size=world,
                           fp8_target=bool(args.fp8_target), arm_reducer=armed)
+    if args.rccl_proxy_cus and trainer.reducer is not None:
+        _install_rccl_proxy(trainer.reducer, args.rccl_proxy_cus, dev)
     # every step's clips and masks are on the device before the first step (below): the next step's
     # target forward may start under the previous step's staged update (JEPATrainer.apply_update)
     trainer.inputs_resident = os.environ.get("VJ_STAGED_UPDATE", "1") == "1"
@@ -328,7 +333,9 @@ def main():
                "clips_per_s_per_gpu": round(value / world, 3), "ms_per_step_median": round(ms_median, 2),
                "clips_per_s_per_gpu_median": round(B / (ms_median * 1e-3), 3),
                "dist_backend": dist.get_backend() if dist.is_initialized() else None,
-               "reducer_armed": armed, "step_tflop": round(flops / 1e12, 2),
+               "reducer_armed": armed, "rccl_proxy_cus": args.rccl_proxy_cus,
+               "rccl_proxy_mode": int(os.environ.get("VJ_RCCL_PROXY_MODE", "0")) if args.rccl_proxy_cus else None,
+               "step_tflop": round(flops / 1e12, 2),
                "step_tflops_per_gpu": round(flops / (ms * 1e-3) / 1e12, 1),
                "mfu_bf16": round(flops / (ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
                "loss_last": round(float(loss.item()), 5), "allreduce_exposed_ms": round(ar_ms, 3),
@@ -340,6 +347,36 @@ def main():
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def _install_rccl_proxy(red, blocks, dev):
+    """--rccl-proxy-cus N: what RCCL's channel kernels cost the step at world > 1,
+    priced on one GPU. Beside every bucket's all-reduce (over a one-rank group RCCL runs no kernel) a
+    copy of twice the bucket's bytes (read + write, the HBM traffic of a ring all-reduce's reduce-scatter
+    and all-gather, 2 (W - 1) / W of the bucket each at W = 8) runs on a stream of its own, on N persistent
+    workgroups (RCCL's channels hold one CU each); the optimizer waits for it, as for the collectives."""
+    from vjepa2_amd import ops
+
+    mode = int(os.environ.get("VJ_RCCL_PROXY_MODE", "0"))  # 1: nt loads / stores, 2: CUs held, no bytes
+    side = torch.cuda.Stream(device=dev)
+    cap = max(b.view.numel() for b in red.buckets + red.tail)
+    cap = (cap + 3) // 4 * 4
+    scratch = torch.empty(2 * cap, device=dev)
+    inner_ar, inner_finish = red._all_reduce, red.finish
+
+    def all_reduce(b):
+        inner_ar(b)
+        side.wait_stream(torch.cuda.current_stream())
+        n = b.view.numel() // 4 * 4  # whole 16-B chunks
+        with torch.cuda.stream(side):
+            for h in range(2):
+                ops.proxy_copy(scratch[h * cap:h * cap + n], b.view[:n], blocks, mode)
+
+    def finish():
+        inner_finish()
+        torch.cuda.current_stream().wait_stream(side)
+
+    red._all_reduce, red.finish = all_reduce, finish
 
 
 def spawn_ranks(n):

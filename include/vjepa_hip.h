@@ -24,6 +24,9 @@ extern "C" {
 #endif
 
 int vj_version(void);
+/* CRC-32 (zlib) of this header as the library was built from it, as an int bit pattern (the binding
+ * refuses a stale build). */
+int vj_header_crc(void);
 int vj_get_last_error(char* buf, size_t n);
 int vj_device_sync(void);
 
@@ -195,6 +198,15 @@ int vj_adamw_ema(long n, float* p, const float* g, float* m, float* v, void* p_b
                  float beta2, float eps, float weight_decay, int step, float grad_scale, const int* found_inf,
                  float* target, void* target_bf16, float momentum, void* stream);
 int vj_cast_bf16(long n, const float* in, void* out, void* stream);
+/* Diagnostic (bench.py --rccl-proxy-cus, no reference counterpart): copy `bytes` (multiple of 16,
+ * 16-B aligned) with `blocks` persistent 256-thread workgroups, standing in for RCCL's channel kernels
+ * holding CUs during the data-parallel gradient all-reduce (app/vjepa/train.py:279-281). mode 0: plain
+ * loads / stores, 1: non-temporal, 2: hold the CUs for the copy's time at 40 GB/s per workgroup, no bytes. */
+int vj_proxy_copy(void* dst, const void* src, long bytes, int blocks, int mode, void* stream);
+/* Persistent GEMM grids launched from now on leave n CUs free (0: every CU): a data-parallel rank sets
+ * it while its gradient all-reduce (app/vjepa/train.py:279-281, RCCL channel kernels) runs beside the
+ * backward. Host state only (no device call). */
+int vj_set_reserved_cus(int n);
 /* dst[c][r] = src[r][c] (bf16; rows, cols, strides multiples of 8): the K-major copy W^T that the
  * data-gradient GEMM dX = dY W (nn.Linear backward) reads as its B operand. */
 int vj_transpose_bf16(int rows, int cols, const void* src, long ld_src, void* dst, long ld_dst, void* stream);

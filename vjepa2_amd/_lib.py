@@ -21,6 +21,7 @@ _F = ctypes.c_float
 # name -> argtypes (restype is always int)
 SIGNATURES = {
     "vj_version": [],
+    "vj_header_crc": [],
     "vj_get_last_error": [ctypes.c_char_p, ctypes.c_size_t],
     "vj_device_sync": [],
     "vj_gemm_bf16": [_I, _I, _I, _P, _L, _I, _P, _L, _I, _I, _P, _P, _L, _P, _L, _P, _L, _P],
@@ -62,6 +63,8 @@ SIGNATURES = {
     "vj_ema": [_L, _P, _P, _F, _P, _P],
     "vj_adamw_ema": [_L, _P, _P, _P, _P, _P, _F, _F, _F, _F, _F, _I, _F, _P, _P, _P, _F, _P],
     "vj_cast_bf16": [_L, _P, _P, _P],
+    "vj_proxy_copy": [_P, _P, _L, _I, _I, _P],
+    "vj_set_reserved_cus": [_I],
     "vj_transpose_bf16": [_I, _I, _P, _L, _P, _L, _P],
     "vj_transpose_bf16_batch": [_I, _P, _L, _P],
     "vj_swiglu_fwd": [_I, _I, _P, _L, _P, _L, _P],
@@ -95,6 +98,19 @@ def load():
             raise RuntimeError(f"{LIB_PATH} does not export {name}: stale build (rebuild the extension)")
         fn.argtypes = args
         fn.restype = ctypes.c_int
+    if not os.environ.get("VJ_LIB"):  # A/B builds of older trees carry their own header
+        import zlib
+
+        hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "vjepa_hip.h")
+        crc_fn = getattr(lib, "vj_header_crc", None)
+        if crc_fn is None:
+            raise RuntimeError(f"{LIB_PATH} predates vj_header_crc: stale build (rebuild the extension)")
+        with open(hdr, "rb") as f:
+            want = zlib.crc32(f.read()) & 0xFFFFFFFF
+        got = crc_fn() & 0xFFFFFFFF
+        if got != want:
+            raise RuntimeError(f"{LIB_PATH} was built from another include/vjepa_hip.h (crc {got:08x}, "
+                               f"header {want:08x}): stale build (rebuild the extension)")
     _lib = lib
     return lib
 

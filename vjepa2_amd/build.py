@@ -35,8 +35,19 @@ def _torch_libdir():
         return None
 
 
+HEADER = os.path.join(os.path.dirname(HERE), "include", "vjepa_hip.h")
+
+
+def header_crc():
+    """CRC-32 of include/vjepa_hip.h (vj_header_crc in the library; checked by _lib.load)."""
+    import zlib
+
+    with open(HEADER, "rb") as f:
+        return zlib.crc32(f.read()) & 0xFFFFFFFF
+
+
 def _needs_build(obj, src, extra=()):
-    deps = [src, *[os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")], *extra]
+    deps = [src, HEADER, *[os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")], *extra]
     return not os.path.exists(obj) or any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 
@@ -47,6 +58,7 @@ def build(verbose=True, force=False, variant=None, defines=()):
     objdir = os.path.join(HERE, "build", variant) if variant else os.path.join(HERE, "build")
     lib = os.path.join(HERE, f"libvjepa_hip_{variant}.so") if variant else LIB
     flags = CFLAGS + [f"-D{d}" for d in defines]
+    flags.append(f"-DVJ_HEADER_CRC={header_crc()}u")
     if variant:
         flags.append("-DVJ_VARIANT_BUILD=1")  # unlocks the timing-only VJ_DIAG_* macros (vj_common.h)
         # experiments: extra compiler flags for every source (e.g. VJ_EXTRA_FLAGS=-fno-slp-vectorize)

@@ -14,6 +14,14 @@ void vj_set_error(const char* fmt, ...) {
 
 extern "C" int vj_version(void) { return 1; }
 
+// CRC-32 of include/vjepa_hip.h when this library was built (build.py passes it): the Python binding
+// compares it with the header it types the entry points from, so a library left stale after a
+// signature change fails loudly instead of taking misplaced arguments.
+#ifndef VJ_HEADER_CRC
+#define VJ_HEADER_CRC 0
+#endif
+extern "C" int vj_header_crc(void) { return (int)(unsigned)VJ_HEADER_CRC; }
+
 extern "C" int vj_get_last_error(char* buf, size_t n) {
   if (!buf || n == 0) return VJ_ERR_ARG;
   strncpy(buf, g_err, n - 1);

@@ -1758,3 +1758,40 @@ extern "C" int vj_video_transform(int B, int T, int H, int W, int C, int S, cons
   VJ_LAUNCH_CHECK("vj_video_transform");
   return VJ_OK;
 }
+
+// ---- RCCL CU-occupancy proxy (diagnostic, bench.py --rccl-proxy-cus): a copy run by `blocks`
+// persistent 256-thread workgroups, one per CU, the way RCCL's channel kernels hold CUs beside the
+// backward's persistent GEMM grids while a bucket is all-reduced at world > 1. 16-B accesses,
+// grid-stride; bytes % 16 == 0. mode 0: plain loads / stores; 1: non-temporal (nt) loads / stores;
+// 2: no memory traffic, every workgroup holds its CU for the time the copy takes at 40 GB/s per
+// workgroup (s_memrealtime, 100 MHz) - separates the CUs held from the bytes moved.
+namespace {
+__global__ __launch_bounds__(256) void k_proxy_copy(long n16, const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                    int mode, long ticks) {
+  if (mode == 2) {
+    const long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+    return;
+  }
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) {
+    if (mode == 1) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = __builtin_nontemporal_load((const u32x4*)(src + i));
+      __builtin_nontemporal_store(v, (u32x4*)(dst + i));
+    } else {
+      dst[i] = src[i];
+    }
+  }
+}
+}  // namespace
+
+extern "C" int vj_proxy_copy(void* dst, const void* src, long bytes, int blocks, int mode, void* stream) {
+  if (bytes == 0) return VJ_OK;
+  VJ_CHECK_ARG(dst && src && bytes > 0 && bytes % 16 == 0 && blocks > 0 && blocks <= 4096 && mode >= 0 && mode <= 2 &&
+                   !(((uintptr_t)dst | (uintptr_t)src) & 15),
+               "vj_proxy_copy: bad arguments (bytes=%ld blocks=%d mode=%d)", bytes, blocks, mode);
+  hipLaunchKernelGGL(k_proxy_copy, dim3(blocks), dim3(256), 0, (hipStream_t)stream, bytes / 16, (const uint4*)src,
+                     (uint4*)dst, mode, bytes / ((long)blocks * 400));
+  VJ_LAUNCH_CHECK("vj_proxy_copy");
+  return VJ_OK;
+}

@@ -62,8 +62,14 @@ class GradReducer:
     """segments: list of (flat_grad_tensor, [(param, offset, numel), ...]) in readiness order.
     Params of `tail_segments` (tiny no-decay arenas) are reduced as one bucket each at finish()."""
 
-    def __init__(self, segments, tail_segments=(), bucket_mb=64, group=None):
+    def __init__(self, segments, tail_segments=(), bucket_mb=64, group=None, reserve_cus=None):
         self.group = group
+        # CUs the persistent GEMM grids leave to RCCL's channel kernels from the first bucket of a
+        # backward to finish() (ops.set_reserved_cus; DESIGN (e)). VJ_RCCL_RESERVE_CUS overrides.
+        if reserve_cus is None:
+            reserve_cus = int(os.environ.get("VJ_RCCL_RESERVE_CUS", "0"))
+        self.reserve_cus = reserve_cus
+        self._reserving = False
         self.world = dist.get_world_size(group)
         self.buckets = []
         cap = int(bucket_mb * (1 << 20)) // 4
@@ -96,6 +102,11 @@ class GradReducer:
         # a backward that raised after queueing buckets must not leave them to fire in the next step
         # (one rank's extra collective would desync the collective order across ranks)
         self._after_join.clear()
+        if getattr(self, "_reserving", False):
+            from . import ops
+
+            ops.set_reserved_cus(0)
+            self._reserving = False
         for b in self.buckets + self.tail:
             b.pending = {id(p) for p in b.params}
             b.work = None
@@ -114,6 +125,11 @@ class GradReducer:
         # bucket order on every rank.
         from . import functions
 
+        if self.reserve_cus and not self._reserving:
+            from . import ops
+
+            ops.set_reserved_cus(self.reserve_cus)
+            self._reserving = True
         if functions.wgrad_stream() is None:
             self._all_reduce(b)
             return
@@ -151,4 +167,9 @@ class GradReducer:
         self._flush()
         for b in self.buckets + self.tail:
             b.work.wait()
+        if self._reserving:
+            from . import ops
+
+            ops.set_reserved_cus(0)
+            self._reserving = False
         self.reset()

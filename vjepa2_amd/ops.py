@@ -681,6 +681,20 @@ def cast_bf16(x, out=None):
     return out
 
 
+def set_reserved_cus(n):
+    """Persistent GEMM grids launched from now on leave n CUs free (vj_set_reserved_cus)."""
+    call("vj_set_reserved_cus", int(n))
+
+
+def proxy_copy(dst, src, blocks, mode=0):
+    """Diagnostic: copy src into dst (same bytes) with `blocks` persistent workgroups (vj_proxy_copy;
+    mode 1: non-temporal, 2: hold the CUs for the copy's time without moving bytes)."""
+    _dev(dst, src)
+    assert dst.is_contiguous() and src.is_contiguous() and dst.numel() * dst.element_size() == src.numel() * src.element_size()
+    _call("vj_proxy_copy", _p(dst), _p(src), src.numel() * src.element_size(), blocks, mode, _stream())
+    return dst
+
+
 # ------------------------------------------------------------------------------------------------
 # fp32-operand parity mode (vj_f32.hip): f32 operands throughout, off the training path.
 

@@ -48,3 +48,16 @@ for case in bk.GEMMS:
         e1 = st[:, it, 1][st[:, it, 1] != 0]
         if len(e1):
             print(f"   tile {it}: epilogue starts spread {np.percentile(e1, 90) - np.percentile(e1, 10):.0f} cyc")
+
+    # S64 interval stamps (K steps 1-4 of each block's second tile; waves 0 and 4): cycles of each
+    # interval between barriers, median over blocks
+    if hasattr(lib, "vj_debug_gemm_istamps"):
+        ib = np.zeros(2048 * 2 * 16, dtype=np.int64)
+        lib.vj_debug_gemm_istamps(ctypes.c_void_p(ib.ctypes.data), ctypes.c_long(ib.nbytes))
+        ib = ib.reshape(2048, 2, 16)
+        ok = (ib[:, 0, :] != 0).all(1)
+        if ok.any():
+            d = np.diff(ib[ok][:, 0, :], axis=1)  # wave 0: intervals after barrier k -> k + 1
+            print(f"   wave 0 intervals (M0, L1, M1, L0', ...) median cycles: {np.median(d, axis=0).astype(int).tolist()}")
+            d4 = np.diff(ib[ok][:, 1, :], axis=1)
+            print(f"   wave 4 intervals median cycles: {np.median(d4, axis=0).astype(int).tolist()}")

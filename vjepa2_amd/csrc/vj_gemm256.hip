@@ -45,17 +45,21 @@ namespace {
 
 #if VJ_GEMM_STAMPS  // diagnostic build: s_memtime per tile (start, main loop done, epilogue done) of wave 0
 __device__ long vj_gemm_stamps[2048 * 16 * 4];
+// S64: s_memtime after each of the 16 barriers of K steps 1-4 of the block's second tile, waves 0 and 4
+__device__ long vj_gemm_istamps[2048 * 2 * 16];
 #endif
 
 // counted wait for this wave's vector-memory operations (LDS-DMA pieces included): at most N in flight
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-  static_assert(N == 0 || N == 4 || N == 8 || N == 12 || N == 16, "vm_wait: add the count");
+  static_assert(N >= 0 && N <= 24 && N % 4 == 0, "vm_wait: add the count");
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
 }
 
 
@@ -139,20 +143,21 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // SB - 1 granules, 4 + 4 x 16 KB = the 4-slot ring's 128 KB, beside the GELU / RoPE tables).
   constexpr bool S64 = STG == 2;
   constexpr int GSZ = 16384;
-  constexpr int SA = 4, SB = 4;
+  // B lead: the waves 4-7 wait for the next K step's B granules at the end of their L1, which at 3
+  // granules of lead stalled on the first K steps of a tile whose panels come from HBM
+  // (profiles/r06_gemm_s64.txt, interval stamps); kernels without an LDS table take 6 B slots
+#ifndef VJ_S64_SB
+#define VJ_S64_SB 6
+#endif
+  constexpr int SA = 4, SB = (EPI == EPI_ROPE || GTAB) ? 4 : VJ_S64_SB;
   constexpr int EA = SA - 1, EB = SB - 1;
   static_assert(EA >= 2 && EB >= 3, "S64 waits assume at least one interval of DMA lead");
   // first row of the wave's rows (S64: the wave's 64-row band in each 128-row half) and the first row
   // of virtual m-tile i relative to it
   constexpr int WRS = S64 ? 64 : WM;
-  // where the S64 loads issue their DMA pieces (VJ_S64_DMA): 0 = one granule in each load interval;
-  // 1 = both groups' two granules in L1 (L0 holds 16 fragment reads, L1 8); 2 = A's in L1, B's split
-#ifndef VJ_S64_DMA
-#define VJ_S64_DMA 0
-#endif
-  constexpr bool S64_AL1 = VJ_S64_DMA >= 1, S64_BL1 = VJ_S64_DMA == 1;
   auto rowoff = [](int i) { return S64 ? (i >> 2) * 128 + (i & 3) * 16 : i * 16; };
   constexpr int RING0 = GTAB ? 32768 : 0;  // LDS offset of the STG ring
+  static_assert(!S64 || (SA + SB) * 16384 + RING0 + ((EPI == EPI_ROPE) ? TAB_BYTES : 0) <= 163840, "S64 rings exceed LDS");
   constexpr int TABB = (NWV == 4 && BMT == 192) ? 0 : TAB_BYTES;  // 2 x 80 KB per CU leaves no table room
   __shared__ __attribute__((aligned(16))) char smem_raw[GTAB ? RING0 + 4 * 32768 : STG && NSL == 5 ? 5 * 32768 : 2 * STAGE + TABB];
   LDS_AS char* smem = (LDS_AS char*)smem_raw;
@@ -366,10 +371,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       dvo[k] = (uint32_t)(gr * dld * 2 + c * 16);
     }
     dma_setup64();
-#pragma unroll
-    for (int i = 0; i < EA; ++i) dma_gran();
-    static_assert(EA == EB, "the prologue issues EA granules on both streams");
-    if (!isA && S64_BL1) dma_gran();  // B all in L1: two K steps (4 granules) ahead
+    for (int i = 0; i < (isA ? EA : EB); ++i) dma_gran();
   } else if constexpr (STG) {
     dma_setup();
 #pragma unroll
@@ -554,7 +556,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // The aux rows of a residual / saved-derivative epilogue (4 loads per lane) are fetched in the last
       // step's L0, after its DMA pieces: the L1 waits after them count 4 more.
       if (wg == run0 + jb) {  // first tile: A position 0 and B positions 0, 1 landed, RoPE table published
-        if (isA || S64_BL1) vm_wait<8>();
+        if (isA) vm_wait<4 * (EA - 1)>();
         else vm_wait<4 * (EB - 2)>();
         __builtin_amdgcn_s_barrier();
         if (wr == 1) __builtin_amdgcn_s_barrier();
@@ -579,6 +581,15 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
             acc[4 * h + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(Ab[i], Bb[j], acc[4 * h + i][j], 0, 0, 0);
       };
       const int qt = q64;  // stream position of this tile's A0 / Blo of step 0
+#if VJ_GEMM_STAMPS
+      long* ist = (stamp_it == 1 && (wave & 3) == 0 && lane == 0 && blockIdx.x < 2048)
+                      ? vj_gemm_istamps + ((long)blockIdx.x * 2 + (wave >> 2)) * 16 : nullptr;
+      auto istamp = [&](int s, int k) {
+        if (ist && s >= 1 && s <= 4) ist[(s - 1) * 4 + k] = __builtin_amdgcn_s_memtime();
+      };
+#else
+      auto istamp = [](int, int) {};
+#endif
       for (int s = 0; s < nks; ++s) {
         const int p = qt + 2 * s;
         const LDS_AS char* sA0 = ring + (p % SA) * GSZ;
@@ -594,24 +605,22 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         for (int i = 0; i < 4; ++i) Ab[i] = frag<true, 128, 64>(sA0, wr * 64 + i * 16, 1, lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) Bb[j] = frag<true, 128, 64>(sB, (wc & 1) * 64 + j * 16, 1, lane);
-        if (isA ? !S64_AL1 : !S64_BL1) dma_gran();
-        if (isA) {
-          if constexpr (S64_AL1) vm_wait<4>();  // A1(s) landed; A0(s + 1) in flight
-          else vm_wait<4 * (EA - 1)>();
-        }
+        dma_gran();
+        if (isA) vm_wait<4 * (EA - 1)>();
         if (AUX && last) stg_aux();
         bar();
+        istamp(s, 0);
         mm64(std::integral_constant<int, 0>{});
         bar();
+        istamp(s, 1);
         // L1
 #pragma unroll
         for (int i = 0; i < 4; ++i) Aa[i] = frag<true, 128, 64>(sA1, wr * 64 + i * 16, 0, lane);
 #pragma unroll
         for (int i = 0; i < 4; ++i) Ab[i] = frag<true, 128, 64>(sA1, wr * 64 + i * 16, 1, lane);
         dma_gran();
-        if (isA ? S64_AL1 : S64_BL1) dma_gran();
         // counts: pieces issued after the awaited granule (+ 4 aux loads in the last step)
-        constexpr int WA = S64_AL1 ? 8 : 4 * (EA - 1), WB = S64_BL1 ? 8 : 4 * (EB - 2);
+        constexpr int WA = 4 * (EA - 1), WB = 4 * (EB - 2);
         if (AUX && last) {
           if (isA) vm_wait<WA + 4>();
           else vm_wait<WB + 4>();
@@ -620,11 +629,13 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
           else vm_wait<WB>();
         }
         bar();
+        istamp(s, 2);
         mm64(std::integral_constant<int, 1>{});
 #if VJ_GEMM_STAMPS
         if (s == 0) st_k1 = __builtin_amdgcn_s_memtime();
 #endif
         if (!last || wr == 0) bar();
+        istamp(s, 3);
       }
       q64 = qt + 2 * nks;
     } else if constexpr (STG) {
@@ -1608,6 +1619,9 @@ extern "C" int vj_qkv_rope_gemm_fp8(int M, int K, const void* A, long lda, const
 extern "C" int vj_debug_gemm_stamps(void* dst, long nbytes) {
   hipMemset(dst, 0, 0);
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(vj_gemm_stamps), nbytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+extern "C" int vj_debug_gemm_istamps(void* dst, long nbytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(vj_gemm_istamps), nbytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
 }
 extern "C" int vj_debug_gemm_stamps_clear() {
   static long z[2048 * 16 * 4];

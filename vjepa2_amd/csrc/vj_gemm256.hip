@@ -143,11 +143,11 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   // SB - 1 granules, 4 + 4 x 16 KB = the 4-slot ring's 128 KB, beside the GELU / RoPE tables).
   constexpr bool S64 = STG == 2;
   constexpr int GSZ = 16384;
-  // B lead: the waves 4-7 wait for the next K step's B granules at the end of their L1, which at 3
-  // granules of lead stalled on the first K steps of a tile whose panels come from HBM
-  // (profiles/r06_gemm_s64.txt, interval stamps); kernels without an LDS table take 6 B slots
+  // B ring depth (variant builds: VJ_S64_SB = 5 / 6 on the kernels without an LDS table). Deeper B
+  // rings removed the DMA stalls of a tile's first K steps (interval stamps) but slowed every later
+  // step: qkv tgt 260 -> 274 us, step -0.6 % (profiles/r06_gemm_s64.txt); 4 kept
 #ifndef VJ_S64_SB
-#define VJ_S64_SB 6
+#define VJ_S64_SB 4
 #endif
   constexpr int SA = 4, SB = (EPI == EPI_ROPE || GTAB) ? 4 : VJ_S64_SB;
   constexpr int EA = SA - 1, EB = SB - 1;

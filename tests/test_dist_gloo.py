@@ -11,7 +11,7 @@ import torch.multiprocessing as mp
 import torch.nn as nn
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap=True):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
         from vjepa2_amd.distributed import GradReducer, init_distributed
@@ -29,7 +29,7 @@ def _worker(rank, world, port, q):
             flat_b[i * 64:(i + 1) * 64] = (rank + 1) * 10.0
         red = GradReducer([(flat_w, [(p, i * 4096, 4096) for i, p in enumerate(weights)])],
                           tail_segments=[(flat_b, [(p, i * 64, 64) for i, p in enumerate(biases)])],
-                          bucket_mb=32e3 / (1 << 20))  # ~2 params per bucket
+                          bucket_mb=32e3 / (1 << 20), overlap=overlap)  # ~2 params per bucket
         order = [4, 3, 1, 0]  # module 2 never reports (unused parameter)
         for i in order:
             red.mark_ready(mods[i])
@@ -45,11 +45,16 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e), None))
 
 
-def test_grad_reducer_two_ranks():
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_grad_reducer_two_ranks(overlap):
+    """overlap=False (VJ_ALLREDUCE=end): every bucket goes out at finish(), same result."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + (os.getpid() % 400)
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    port = 29500 + (os.getpid() % 400) + (0 if overlap else 401)
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for p in ps:
         p.start()
     res = [q.get(timeout=120) for _ in ps]

@@ -1491,7 +1491,13 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
     return launch2w(epi, g, st);
   }
   if (bn == 256) {
-    if (a_kmajor && b_kmajor && use_bm192(M, tn)) {
+    // 192-row tiles run the one-tile main loop; where S64 can run instead (K % 64 == 0) the 256-row S64
+    // tiles measured +0.2 % per step over the cost model's 192-row picks (the context GEMMs;
+    // VJ_GEMM_BM192=0 vs default, two same-call runs each, profiles/r06_gemm_s64.txt).
+    // VJ_GEMM_BM192=1 still forces them.
+    const char* bm = getenv("VJ_GEMM_BM192");
+    const bool s64_ok = a_kmajor && b_kmajor && use_stg(K, epi) == 2 && !(bm && bm[0] == '1');
+    if (a_kmajor && b_kmajor && !s64_ok && use_bm192(M, tn)) {
       g.tiles_m = vj_cdiv(M, 192);
       g.group = tile_group(g.tiles_m, tn);
       return launch192(epi, g, st);

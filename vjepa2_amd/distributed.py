@@ -62,8 +62,15 @@ class GradReducer:
     """segments: list of (flat_grad_tensor, [(param, offset, numel), ...]) in readiness order.
     Params of `tail_segments` (tiny no-decay arenas) are reduced as one bucket each at finish()."""
 
-    def __init__(self, segments, tail_segments=(), bucket_mb=64, group=None, reserve_cus=None):
+    def __init__(self, segments, tail_segments=(), bucket_mb=64, group=None, reserve_cus=None, overlap=None):
         self.group = group
+        # overlap=False (VJ_ALLREDUCE=end): every bucket is issued at finish(), after the backward,
+        # instead of as soon as its last layer is done. The collectives are then exposed (~1.30 GB per
+        # step at RCCL's bus bandwidth) but never share the CUs with the backward's kernels, which on
+        # one GPU cost about 2.5x the CU-time they hold (DESIGN (e), profiles/r06_rccl_proxy_ab.txt).
+        if overlap is None:
+            overlap = os.environ.get("VJ_ALLREDUCE", "overlap") != "end"
+        self.overlap = overlap
         # CUs the persistent GEMM grids leave to RCCL's channel kernels from the first bucket of a
         # backward to finish() (ops.set_reserved_cus; DESIGN (e)). VJ_RCCL_RESERVE_CUS overrides.
         if reserve_cus is None:
@@ -143,7 +150,7 @@ class GradReducer:
 
     def mark_ready(self, module):
         """Hook called when `module`'s backward has finished writing its parameter gradients."""
-        if not self.armed:
+        if not self.armed or not self.overlap:
             return
         for p in module.parameters():
             i = self.owner.get(id(p))

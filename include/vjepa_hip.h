@@ -87,6 +87,19 @@ int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, in
                    long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
                    const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
                    const float* cos_t, const float* sin_t, int fblk, void* stream);
+/* With attention dropout (F.scaled_dot_product_attention(..., dropout_p=self.proj_drop_prob),
+ * src/models/utils/modules.py:246 / 370 / 417; applied whether or not the module is training, as there):
+ * score (query token t, head h, key j of its sequence) is kept iff
+ * drop_u(drop_row(seed, t*H + h), j) >= round(p * 2^32) (the hash of vj_dropout below); the kept
+ * probabilities are scaled by 1 / (1 - p) and stats[0] stays the log-sum-exp of the undropped scores.
+ * The backward regenerates the mask: it must get the forward's p and seed. p = 0: vj_attn_*_fc. */
+int vj_attn_fwd_ex(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o, long ldo,
+                   float* stats, float scale, int ngroups, const int* nseq, const int* len, int fblk, float dropout_p,
+                   unsigned seed, void* stream);
+int vj_attn_bwd_ex(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, const void* o,
+                   long ldo, const void* dout, long lddo, float* stats, void* dqkv, long ldd, float scale, int ngroups,
+                   const int* nseq, const int* len, const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr,
+                   const float* cos_t, const float* sin_t, int fblk, float dropout_p, unsigned seed, void* stream);
 
 /* Fused QKV projection + RoPE of q and k: C[M, 3*H*hd] (bf16) = A[M,K] W[3*H*hd, K]^T + bias, then
  * q, k columns rotated (modules.py:330 + 343-365) in the GEMM epilogue. Same RoPE arguments as vj_rope;
@@ -231,6 +244,16 @@ int vj_swiglu_bwd(int M, int h, const void* dh, long lddh, const void* x12, long
 int vj_rowscale_add(int M, int N, const float* y, long ldy, const float* scale, const void* resid, long ldr, void* out,
                     long ldo, int bf16_resid, void* stream);
 int vj_rowscale_bf16(int M, int N, const float* dx, long ld, const float* scale, void* out, long ldo, void* stream);
+/* Dropout (nn.Dropout: MLP.drop after the activation and after fc2, modules.py:75-82; proj_drop after
+ * the attention projection, :257 / :381), on [M][N]: element (m, n) is kept iff
+ * drop_u(drop_row(seed, m), n) >= round(p * 2^32), with drop_mix = the "lowbias32" integer hash,
+ * drop_row(s, r) = drop_mix(s ^ (r * 0x9e3779b1)), drop_u(k, c) = drop_mix(k + c * 0x85ebca77) (uint32
+ * arithmetic). y = bf16(bf16(x) * z), z = 1 / (1 - p) if kept else 0; x f32 (x_f32 = 1) or bf16.
+ * out = y (bf16); with resid: out = resid + y (f32, or bf16 when resid_f32 = 0); with aux (bf16):
+ * out = bf16(y * aux). The backward of a dropout is the same call on the gradient with the same seed.
+ * N, strides multiples of 4; p in [0, 1). */
+int vj_dropout(int M, int N, const void* x, long ldx, int x_f32, const void* aux, long ldaux, const void* resid,
+               long ldr, int resid_f32, void* out, long ldo, float dropout_p, unsigned seed, void* stream);
 
 /* JEPA multi-block 3-D masks on the device (src/masks/multiseq_multiblock3d.py:155-239): the host
  * makes the reference's RNG draws (block size, (start, top, left) per block: boxes int32

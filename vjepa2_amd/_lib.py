@@ -17,6 +17,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_long
 _F = ctypes.c_float
+_U = ctypes.c_uint
 
 # name -> argtypes (restype is always int)
 SIGNATURES = {
@@ -32,6 +33,9 @@ SIGNATURES = {
     "vj_attn_fwd_fc": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _F, _I, _P, _P, _I, _P],
     "vj_attn_bwd_fc": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _F, _I, _P, _P, _P, _I, _I, _I, _P,
                        _P, _I, _P],
+    "vj_attn_fwd_ex": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _F, _I, _P, _P, _I, _F, _U, _P],
+    "vj_attn_bwd_ex": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _F, _I, _P, _P, _P, _I, _I, _I, _P,
+                       _P, _I, _F, _U, _P],
     "vj_qkv_rope_gemm": [_I, _I, _P, _L, _P, _L, _P, _P, _L, _I, _I, _P, _I, _I, _I, _P, _P, _I, _P],
     "vj_layernorm_fwd": [_I, _I, _P, _I, _L, _P, _P, _F, _P, _I, _L, _P, _P, _P],
     "vj_gemm_fp8": [_I, _I, _I, _P, _L, _P, _P, _L, _P, _I, _P, _P, _L, _P, _L, _P, _L, _P],
@@ -71,6 +75,7 @@ SIGNATURES = {
     "vj_swiglu_bwd": [_I, _I, _P, _L, _P, _L, _P, _L, _P],
     "vj_rowscale_add": [_I, _I, _P, _L, _P, _P, _L, _P, _L, _I, _P],
     "vj_rowscale_bf16": [_I, _I, _P, _L, _P, _P, _L, _P],
+    "vj_dropout": [_I, _I, _P, _L, _I, _P, _L, _P, _L, _I, _P, _L, _F, _U, _P],
     "vj_xattn_ws_floats": [_I, _I, _I, _I, _I, ctypes.POINTER(_L)],
     "vj_xattn_fwd": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _P, _F, _P, _L, _P],
     "vj_xattn_bwd": [_I, _I, _I, _I, _I, _P, _L, _P, _L, _P, _L, _P, _L, _P, _F, _P, _L, _P, _L, _P, _L, _P],

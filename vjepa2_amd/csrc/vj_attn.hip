@@ -81,6 +81,11 @@ struct AttnArgs {
   // (build_action_block_causal_attention_mask, modules.py:12-23, with fblk = cond tokens + H*W);
   // 0 = non-causal (every key of the sequence)
   int fblk;
+  // dropout on the attention probabilities (F.scaled_dot_product_attention dropout_p, modules.py:246,
+  // 370, 417): score (query token t, head h, key j of the sequence) is kept iff
+  // drop_u(drop_row(drop_seed, t * H + h), j) >= drop_thresh, kept probabilities scaled by drop_scale
+  uint32_t drop_thresh, drop_seed;
+  float drop_scale;
 };
 
 // key limit of query qloc (keys [0, klim) are visible) and its block-uniform bounds
@@ -344,7 +349,7 @@ __device__ __forceinline__ void wave_store_rows(const f32x16 (&x)[Hd<HD>::P / 32
 
 // ------------------------------------------------------------------------------------------------
 // Forward: block = 4 waves x 32 queries, KV tiles of 64 keys double-buffered in LDS.
-template <int HD>
+template <int HD, bool DROP>
 __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr int KT = 64;
@@ -364,6 +369,7 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
   const int klim = fc_klim(a.fblk, qloc, len);
   const int kend = fc_klim(a.fblk, min(qt * 128 + 127, len - 1), len);
   const int kmask0 = fc_klim(a.fblk, qt * 128, len);
+  [[maybe_unused]] const uint32_t drow = DROP ? drop_row(a.drop_seed, (uint32_t)((seq0 + qloc) * a.H + h)) : 0u;
 
   // Q^T fragments (B operand of S^T = K Q^T): lane holds Q[q][16s + 8h + j] (zero past HD).
   bf16x8 qf[HDP / 16];
@@ -514,6 +520,13 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
       }
     }
     lsum += ls;
+    if constexpr (DROP) {  // l sums every p; the PV product takes the kept ones (x drop_scale at the end)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (drop_u(drow, (uint32_t)(kb + kk * 32 + acc_row(r, lane))) < a.drop_thresh) st[kk][r] = 0.f;
+    }
     // O^T += V^T P^T over 4 key-steps of 16
     lds_wait();
     {
@@ -538,7 +551,7 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
     if (kt0 + 1 < nkt) tile_iter(kt0 + 1, I0{}, std::false_type{});
   }
   const float l_tot = sum_xor32(lsum);
-  const float inv = 1.f / l_tot;
+  const float inv = DROP ? a.drop_scale / l_tot : 1.f / l_tot;
   if constexpr (HD == 32) {
     // head dim 32 (5 workgroups per CU): the direct 4-B stores measured faster than the LDS image
     // (predictor forward 269 vs 278 us, profiles/r05_attn_row_stores_ab.txt)
@@ -561,7 +574,7 @@ __global__ __launch_bounds__(256, (HD <= 64 ? FWD_OCC : 2)) void k_attn_fwd(Attn
 // dK/dV: block = 4 waves x (32 KW) keys; sweep query tiles of 32 (Q, dO, lse, delta staged in LDS).
 // Each wave owns KW 32-key tiles (key tile kw of wave w: keys kw*128 + w*32 + 0..31 of the block),
 // so every staged Q / dO fragment feeds KW independent MFMA chains per barrier.
-template <int HD, int KW>
+template <int HD, int KW, bool DROP>
 __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr int QT = 32;
@@ -662,14 +675,16 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
     // S - lse2/c = Q K^T - lse2/c (rows: queries, col: key); dP - delta = dO V^T - delta: the
     // per-query terms are the accumulators' initial values, so no per-row registers stay live
     f32x16 sacc[KW], dp[KW];
+    [[maybe_unused]] float dlr[DROP ? 16 : 1];  // dropout: -delta per query row (dS = p (z dP - delta))
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = acc_row(r, lane);
       const float l2 = Ls[qi] * rc, dl = Ls[32 + qi];
+      if constexpr (DROP) dlr[r] = dl;
 #pragma unroll
       for (int kw = 0; kw < KW; ++kw) {
         sacc[kw][r] = l2;
-        dp[kw][r] = dl;
+        dp[kw][r] = DROP ? 0.f : dl;
       }
     }
 #pragma unroll
@@ -697,15 +712,30 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
         for (int r = 0; r < 16; ++r)
           if (qt * QT + acc_row(r, lane) < qlo[kw]) sacc[kw][r] = -INFINITY;
     }
-    // P = 2^(c*S - lse2); dS = P * (dP - delta)
-#pragma unroll
-    for (int kw = 0; kw < KW; ++kw)
+    // P = 2^(c*S - lse2); dS = P * (dP - delta). Dropout (z = drop_scale or 0): dV takes P z, and
+    // dS = P (z dP - delta), dP = dO V^T being the gradient of the dropped probabilities
+    if constexpr (DROP) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(sacc[kw][r] * c);
-        sacc[kw][r] = p;
-        dp[kw][r] *= p;
+        const uint32_t rk = drop_row(a.drop_seed, (uint32_t)((seq0 + qt * QT + acc_row(r, lane)) * a.H + h));
+#pragma unroll
+        for (int kw = 0; kw < KW; ++kw) {
+          const float p = __builtin_amdgcn_exp2f(sacc[kw][r] * c);
+          const float z = drop_u(rk, (uint32_t)kloc[kw]) >= a.drop_thresh ? a.drop_scale : 0.f;
+          dp[kw][r] = p * fmaf(z, dp[kw][r], dlr[r]);
+          sacc[kw][r] = p * z;
+        }
       }
+    } else {
+#pragma unroll
+      for (int kw = 0; kw < KW; ++kw)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(sacc[kw][r] * c);
+          sacc[kw][r] = p;
+          dp[kw][r] *= p;
+        }
+    }
     // dV^T += dO^T P ; dK^T += Q^T dS   (k-permuted accumulators as B operands)
     lds_wait();
 #pragma unroll
@@ -758,7 +788,7 @@ __global__ __launch_bounds__(256) void k_attn_bwd_dkdv(AttnArgs a) {
 // fragment read from LDS feeds QW independent MFMA chains.
 // It runs first and computes delta = rowsum(dO * O) itself (from its dO fragments and O), writing
 // -delta to stats for the dK/dV sweep.
-template <int HD, int QW>
+template <int HD, int QW, bool DROP>
 __global__ __launch_bounds__(256, (HD == 64 ? DQ64_OCC : 1)) void k_attn_bwd_dq(AttnArgs a) {
   constexpr int HDP = Hd<HD>::P;
   constexpr int KT = 64;
@@ -814,6 +844,9 @@ __global__ __launch_bounds__(256, (HD == 64 ? DQ64_OCC : 1)) void k_attn_bwd_dq(
 #pragma unroll
       for (int r = 0; r < 16; ++r) dqt[qw][d][r] = 0.f;
   const float c = a.scale * LOG2E;
+  [[maybe_unused]] uint32_t drow[QW];
+#pragma unroll
+  for (int qw = 0; qw < QW; ++qw) drow[qw] = DROP ? drop_row(a.drop_seed, (uint32_t)((seq0 + qloc[qw]) * a.H + h)) : 0u;
   float nl2[QW];  // -lse2 / c: initial value of the S^T accumulators, so p = 2^(c * acc)
 #pragma unroll
   for (int qw = 0; qw < QW; ++qw) nl2[qw] = -lse2[qw] / c;
@@ -872,7 +905,7 @@ __global__ __launch_bounds__(256, (HD == 64 ? DQ64_OCC : 1)) void k_attn_bwd_dq(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           st[qw][r] = nl2[qw];
-          dpt[qw][r] = dl[qw];
+          dpt[qw][r] = DROP ? 0.f : dl[qw];
         }
 #pragma unroll
       for (int s = 0; s < HDP / 16; ++s)
@@ -894,7 +927,16 @@ __global__ __launch_bounds__(256, (HD == 64 ? DQ64_OCC : 1)) void k_attn_bwd_dq(
 #pragma unroll
       for (int qw = 0; qw < QW; ++qw)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dpt[qw][r] *= __builtin_amdgcn_exp2f(st[qw][r] * c);
+        for (int r = 0; r < 16; ++r) {
+          const float p = __builtin_amdgcn_exp2f(st[qw][r] * c);
+          if constexpr (DROP) {  // dS = P (z dP - delta), dP = dO V^T (see k_attn_bwd_dkdv)
+            const uint32_t kl = (uint32_t)(kt * KT + kk * 32 + acc_row(r, lane));
+            const float z = drop_u(drow[qw], kl) >= a.drop_thresh ? a.drop_scale : 0.f;
+            dpt[qw][r] = p * fmaf(z, dpt[qw][r], dl[qw]);
+          } else {
+            dpt[qw][r] *= p;
+          }
+        }
       lds_wait();
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) tie(ktf[s2]);
@@ -968,48 +1010,65 @@ int check_common(int H, int hd, long ld, long ldo) {
 
 }  // namespace
 
-extern "C" int vj_attn_fwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+// Forward / backward with SDPA's attention dropout (dropout_p = p, modules.py:246 / 370 / 417; p = 0 is
+// the plain kernels): the mask is regenerated from `seed` by the backward, which must get the same p and
+// seed as the forward it differentiates.
+extern "C" int vj_attn_fwd_ex(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
                               void* o, long ldo, float* lse_stats, float scale, int ngroups, const int* nseq,
-                              const int* len, int fblk, void* stream) {
+                              const int* len, int fblk, float dropout_p, unsigned seed, void* stream) {
   if (T == 0) return VJ_OK;
   int rc = check_common(H, hd, ld, ldo);
   if (rc) return rc;
   VJ_CHECK_ARG(fblk >= 0, "vj_attn_fwd: bad frame block %d", fblk);
+  VJ_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "vj_attn_fwd: dropout_p must be in [0, 1)");
   AttnArgs a{};
   a.fblk = fblk;
   a.qkv = (const bf16_t*)qkv; a.ld = ld; a.q_off = q_off; a.k_off = k_off; a.v_off = v_off;
   a.o = (bf16_t*)o; a.ldo = ldo; a.stats = lse_stats; a.H = H; a.T = T; a.scale = scale;
+  a.drop_thresh = vj_drop_thresh(dropout_p); a.drop_seed = seed; a.drop_scale = 1.f / (1.f - dropout_p);
   rc = fill_groups(a.sg, ngroups, nseq, len, 128, T);
   if (rc) return rc;
   dim3 grid(a.sg.tiles_prefix[MAXG], H);
   hipStream_t st = (hipStream_t)stream;
-  switch (hd) {
-    case 64: hipLaunchKernelGGL(k_attn_fwd<64>, grid, dim3(256), 0, st, a); break;
-    case 32: hipLaunchKernelGGL(k_attn_fwd<32>, grid, dim3(256), 0, st, a); break;
-    case 80: hipLaunchKernelGGL(k_attn_fwd<80>, grid, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL(k_attn_fwd<88>, grid, dim3(256), 0, st, a); break;
-  }
+  auto go = [&](auto drop_c) {
+    constexpr bool D = decltype(drop_c)::value;
+    switch (hd) {
+      case 64: hipLaunchKernelGGL((k_attn_fwd<64, D>), grid, dim3(256), 0, st, a); break;
+      case 32: hipLaunchKernelGGL((k_attn_fwd<32, D>), grid, dim3(256), 0, st, a); break;
+      case 80: hipLaunchKernelGGL((k_attn_fwd<80, D>), grid, dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL((k_attn_fwd<88, D>), grid, dim3(256), 0, st, a); break;
+    }
+  };
+  if (a.drop_thresh) go(std::true_type{});
+  else go(std::false_type{});
   VJ_LAUNCH_CHECK("vj_attn_fwd");
   return VJ_OK;
+}
+
+extern "C" int vj_attn_fwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                              void* o, long ldo, float* lse_stats, float scale, int ngroups, const int* nseq,
+                              const int* len, int fblk, void* stream) {
+  return vj_attn_fwd_ex(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, lse_stats, scale, ngroups, nseq, len, fblk,
+                        0.f, 0u, stream);
 }
 
 extern "C" int vj_attn_fwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off, void* o,
                            long ldo, float* lse_stats, float scale, int ngroups, const int* nseq, const int* len,
                            void* stream) {
-  return vj_attn_fwd_fc(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, lse_stats, scale, ngroups, nseq, len, 0,
-                        stream);
+  return vj_attn_fwd_ex(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, lse_stats, scale, ngroups, nseq, len, 0, 0.f,
+                        0u, stream);
 }
 
-
-extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+extern "C" int vj_attn_bwd_ex(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
                               const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
                               long ldd, float scale, int ngroups, const int* nseq, const int* len,
                               const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t,
-                              const float* sin_t, int fblk, void* stream) {
+                              const float* sin_t, int fblk, float dropout_p, unsigned seed, void* stream) {
   if (T == 0) return VJ_OK;
   int rc = check_common(H, hd, ld, ldo);
   if (rc) return rc;
   VJ_CHECK_ARG(fblk >= 0, "vj_attn_bwd: bad frame block %d", fblk);
+  VJ_CHECK_ARG(dropout_p >= 0.f && dropout_p < 1.f, "vj_attn_bwd: dropout_p must be in [0, 1)");
   VJ_CHECK_ARG(lddo % 8 == 0 && ldd % 8 == 0, "vj_attn_bwd: strides must be multiples of 8");
   VJ_CHECK_ARG(!cos_t || (sin_t && (rope_ids || rope_mod > 0) && rope_tpf > 0 && rope_tpr > 0),
                "vj_attn_bwd: incomplete RoPE arguments");
@@ -1024,6 +1083,7 @@ extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, in
   a.qkv = (const bf16_t*)qkv; a.ld = ld; a.q_off = q_off; a.k_off = k_off; a.v_off = v_off;
   a.o = (bf16_t*)o; a.ldo = ldo; a.dout = (const bf16_t*)dout; a.lddo = lddo; a.stats = stats;
   a.dqkv = (bf16_t*)dqkv; a.ldd = ldd; a.H = H; a.T = T; a.scale = scale; a.fblk = fblk;
+  a.drop_thresh = vj_drop_thresh(dropout_p); a.drop_seed = seed; a.drop_scale = 1.f / (1.f - dropout_p);
   // key / query 32-row tiles per wave of the two sweeps (block tile = 128 x that)
   const int kw = hd == 32 ? KW32 : hd == 64 ? KW64 : 1;
   const int qw = hd == 32 ? QW32 : hd == 64 ? QW64 : 1;
@@ -1035,26 +1095,40 @@ extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, in
   hipStream_t st = (hipStream_t)stream;
   const dim3 gk(ak.sg.tiles_prefix[MAXG], H), gq(aq.sg.tiles_prefix[MAXG], H);
   // dQ sweep first: it writes -delta for the dK/dV sweep
-  switch (hd) {
-    case 64:
-      hipLaunchKernelGGL((k_attn_bwd_dq<64, QW64>), gq, dim3(256), 0, st, aq);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<64, KW64>), gk, dim3(256), 0, st, ak);
-      break;
-    case 32:
-      hipLaunchKernelGGL((k_attn_bwd_dq<32, QW32>), gq, dim3(256), 0, st, aq);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<32, KW32>), gk, dim3(256), 0, st, ak);
-      break;
-    case 80:
-      hipLaunchKernelGGL((k_attn_bwd_dq<80, 1>), gq, dim3(256), 0, st, aq);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<80, 1>), gk, dim3(256), 0, st, ak);
-      break;
-    default:
-      hipLaunchKernelGGL((k_attn_bwd_dq<88, 1>), gq, dim3(256), 0, st, aq);
-      hipLaunchKernelGGL((k_attn_bwd_dkdv<88, 1>), gk, dim3(256), 0, st, ak);
-      break;
-  }
+  auto go = [&](auto drop_c) {
+    constexpr bool D = decltype(drop_c)::value;
+    switch (hd) {
+      case 64:
+        hipLaunchKernelGGL((k_attn_bwd_dq<64, QW64, D>), gq, dim3(256), 0, st, aq);
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<64, KW64, D>), gk, dim3(256), 0, st, ak);
+        break;
+      case 32:
+        hipLaunchKernelGGL((k_attn_bwd_dq<32, QW32, D>), gq, dim3(256), 0, st, aq);
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<32, KW32, D>), gk, dim3(256), 0, st, ak);
+        break;
+      case 80:
+        hipLaunchKernelGGL((k_attn_bwd_dq<80, 1, D>), gq, dim3(256), 0, st, aq);
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<80, 1, D>), gk, dim3(256), 0, st, ak);
+        break;
+      default:
+        hipLaunchKernelGGL((k_attn_bwd_dq<88, 1, D>), gq, dim3(256), 0, st, aq);
+        hipLaunchKernelGGL((k_attn_bwd_dkdv<88, 1, D>), gk, dim3(256), 0, st, ak);
+        break;
+    }
+  };
+  if (a.drop_thresh) go(std::true_type{});
+  else go(std::false_type{});
   VJ_LAUNCH_CHECK("vj_attn_bwd");
   return VJ_OK;
+}
+
+extern "C" int vj_attn_bwd_fc(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
+                              const void* o, long ldo, const void* dout, long lddo, float* stats, void* dqkv,
+                              long ldd, float scale, int ngroups, const int* nseq, const int* len,
+                              const int* rope_ids, int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t,
+                              const float* sin_t, int fblk, void* stream) {
+  return vj_attn_bwd_ex(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
+                        nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, fblk, 0.f, 0u, stream);
 }
 
 extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q_off, int k_off, int v_off,
@@ -1062,6 +1136,6 @@ extern "C" int vj_attn_bwd(int T, int H, int hd, const void* qkv, long ld, int q
                            float scale, int ngroups, const int* nseq, const int* len, const int* rope_ids,
                            int rope_mod, int rope_tpf, int rope_tpr, const float* cos_t, const float* sin_t,
                            void* stream) {
-  return vj_attn_bwd_fc(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
-                        nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, 0, stream);
+  return vj_attn_bwd_ex(T, H, hd, qkv, ld, q_off, k_off, v_off, o, ldo, dout, lddo, stats, dqkv, ldd, scale, ngroups,
+                        nseq, len, rope_ids, rope_mod, rope_tpf, rope_tpr, cos_t, sin_t, 0, 0.f, 0u, stream);
 }

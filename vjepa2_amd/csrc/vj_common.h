@@ -216,3 +216,22 @@ __device__ __forceinline__ uint32_t clamp_u31(long b) {
   if (b < 0) return 0;
   return b > 0x7fffffffL ? 0x7fffffffu : (uint32_t)b;
 }
+
+// ----- dropout keep masks (nn.Dropout / F.scaled_dot_product_attention dropout_p, modules.py:75-82,
+// 246, 257, 370, 381): a counter-based hash of (seed, row, column), so the backward regenerates the
+// forward's mask from the seed alone. Element (row r, column c) of a call with seed s is kept iff
+// drop_u(drop_row(s, r), c) >= thresh, thresh = round(p * 2^32); kept values are scaled by 1 / (1 - p).
+// Rows: the token row of an activation, or token * H + head of an attention score row (query token);
+// columns: the feature, or the key's index in its sequence. Restated for the tests in
+// tests/test_dropout.py (vj_dropout_mask_ref).
+__device__ __forceinline__ uint32_t drop_mix(uint32_t x) {  // "lowbias32" integer hash
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t drop_row(uint32_t seed, uint32_t row) { return drop_mix(seed ^ (row * 0x9e3779b1u)); }
+__device__ __forceinline__ uint32_t drop_u(uint32_t rowkey, uint32_t col) { return drop_mix(rowkey + col * 0x85ebca77u); }
+uint32_t vj_drop_thresh(float p);  // round(p * 2^32), saturated (vj_variants.hip)

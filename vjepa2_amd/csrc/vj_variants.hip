@@ -5,7 +5,10 @@
 //    pass its gradients (dx1 | dx2, again side by side: the two weight-gradient GEMMs read halves);
 //  * stochastic depth (timm drop_path via DropPath, modules.py:53-64, applied at :561-562): a
 //    per-sample factor (0 or 1 / keep) on the branch output before the residual add, and on the
-//    branch's output gradient in the backward.
+//    branch's output gradient in the backward;
+//  * dropout (nn.Dropout: MLP.drop after the activation and after fc2, modules.py:75-82; proj_drop
+//    after the attention projection, :257 / :381): the element mask of vj_common.h's drop_row /
+//    drop_u, so the backward (the same mask times the incoming gradient) needs only the seed.
 // Rounding follows the reference under bf16 autocast (app/vjepa/train.py:438): every intermediate
 // the reference materialises in bf16 is rounded to bf16 here at the same point; the arithmetic
 // between roundings is f32, as in PyTorch's elementwise kernels (opmath = float).
@@ -114,7 +117,93 @@ __global__ void k_rowscale_bf16(int M, int n4, const float* __restrict__ dx, lon
   }
 }
 
+// Dropout, elementwise (F.dropout in the branch's bf16 under autocast: y = bf16(bf16(x) * z) with
+// z = 1 / (1 - p) on kept elements, 0 on dropped ones; the backward is the same op on the gradient).
+// MODE 0: out = y (bf16); 1: out = resid + y (f32 residual stream); 2: the same on a bf16 residual;
+// 3: out = bf16(y * aux) (aux bf16: GELU'(pre), the activation's backward after the dropout's).
+template <bool XF32, int MODE>
+__global__ void k_dropout(int M, int n4, const void* __restrict__ x, long ldx, const bf16_t* __restrict__ aux,
+                          long lda, const void* __restrict__ resid, long ldr, void* __restrict__ out, long ldo,
+                          uint32_t thresh, float scale, uint32_t seed) {
+  const long n = (long)M * n4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long m = i / n4;
+    const int c = (int)(i - m * n4) * 4;
+    float v[4];
+    if constexpr (XF32) {
+      const float4 t = *(const float4*)((const float*)x + m * ldx + c);
+      v[0] = bfr(t.x); v[1] = bfr(t.y); v[2] = bfr(t.z); v[3] = bfr(t.w);
+    } else {
+      const uint2 t = *(const uint2*)((const bf16_t*)x + m * ldx + c);
+      v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+      v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+    }
+    const uint32_t rk = drop_row(seed, (uint32_t)m);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = bfr(v[j] * (drop_u(rk, (uint32_t)(c + j)) >= thresh ? scale : 0.f));
+    if constexpr (MODE == 3) {
+      const uint2 t = *(const uint2*)(aux + m * lda + c);
+      v[0] *= __uint_as_float(t.x << 16); v[1] *= __uint_as_float(t.x & 0xffff0000u);
+      v[2] *= __uint_as_float(t.y << 16); v[3] *= __uint_as_float(t.y & 0xffff0000u);
+    }
+    if constexpr (MODE == 1) {
+      const float4 r = *(const float4*)((const float*)resid + m * ldr + c);
+      *(float4*)((float*)out + m * ldo + c) = make_float4(r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]);
+    } else {
+      if constexpr (MODE == 2) {
+        const uint2 r = *(const uint2*)((const bf16_t*)resid + m * ldr + c);
+        v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
+        v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
+      }
+      *(uint2*)((bf16_t*)out + m * ldo + c) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+    }
+  }
+}
+
 }  // namespace
+
+uint32_t vj_drop_thresh(float p) {
+  const double t = (double)p * 4294967296.0;
+  return t <= 0.0 ? 0u : (t >= 4294967295.0 ? 4294967295u : (uint32_t)(t + 0.5));
+}
+
+extern "C" int vj_dropout(int M, int N, const void* x, long ldx, int x_f32, const void* aux, long ldaux,
+                          const void* resid, long ldr, int resid_f32, void* out, long ldo, float p, unsigned seed,
+                          void* stream) {
+  if (M == 0 || N == 0) return VJ_OK;
+  VJ_CHECK_ARG(M > 0 && N > 0 && x && out && !(aux && resid), "vj_dropout: bad arguments");
+  VJ_CHECK_ARG(p >= 0.f && p < 1.f, "vj_dropout: p must be in [0, 1) (got %g)", (double)p);
+  VJ_CHECK_ARG(N % 4 == 0 && ldx % 4 == 0 && ldo % 4 == 0 && (!aux || ldaux % 4 == 0) && (!resid || ldr % 4 == 0) &&
+                   !((uintptr_t)x & (x_f32 ? 15 : 7)) && !((uintptr_t)aux & 7) &&
+                   !((uintptr_t)resid & (resid_f32 ? 15 : 7)) && !((uintptr_t)out & (resid && resid_f32 ? 15 : 7)),
+               "vj_dropout: N, strides must be multiples of 4 and the rows aligned");
+  const int n4 = N / 4;
+  const uint32_t th = vj_drop_thresh(p);
+  const float sc = 1.f / (1.f - p);
+  const dim3 g(stream_blocks((long)M * n4)), b(256);
+  hipStream_t st = (hipStream_t)stream;
+  const int mode = resid ? (resid_f32 ? 1 : 2) : (aux ? 3 : 0);
+#define VJ_DROP_LAUNCH(XF, MD) \
+  hipLaunchKernelGGL((k_dropout<XF, MD>), g, b, 0, st, M, n4, x, ldx, (const bf16_t*)aux, ldaux, resid, ldr, out, ldo, th, sc, seed)
+  if (x_f32) {
+    switch (mode) {
+      case 0: VJ_DROP_LAUNCH(true, 0); break;
+      case 1: VJ_DROP_LAUNCH(true, 1); break;
+      case 2: VJ_DROP_LAUNCH(true, 2); break;
+      default: VJ_DROP_LAUNCH(true, 3); break;
+    }
+  } else {
+    switch (mode) {
+      case 0: VJ_DROP_LAUNCH(false, 0); break;
+      case 1: VJ_DROP_LAUNCH(false, 1); break;
+      case 2: VJ_DROP_LAUNCH(false, 2); break;
+      default: VJ_DROP_LAUNCH(false, 3); break;
+    }
+  }
+#undef VJ_DROP_LAUNCH
+  VJ_LAUNCH_CHECK("vj_dropout");
+  return VJ_OK;
+}
 
 extern "C" int vj_swiglu_fwd(int M, int h, const void* x12, long ld, void* out, long ldo, void* stream) {
   if (M == 0 || h == 0) return VJ_OK;

@@ -191,8 +191,8 @@ def block_forward_fp8(x, blk, lay):
     scaled e4m3; attention, proj and fc2 stay bf16 (their inputs come out of the attention / GELU
     kernels, whose rows span many tiles). f32 residual stream as in block_forward."""
     attn, mlp = blk.attn, blk.mlp
-    if getattr(mlp, "swiglu", False) or _drop_scales(blk, lay, x.device) is not None:
-        raise NotImplementedError("the fp8 block path covers the GELU MLP without drop_path")
+    if getattr(mlp, "swiglu", False) or _drop_scales(blk, lay, x.device) is not None or _has_dropout(blk):
+        raise NotImplementedError("the fp8 block path covers the GELU MLP without drop_path / dropout")
     H = attn.num_heads
     hd = x.shape[1] // H
     ln1, e1 = ops.layernorm_fwd_fp8(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps)
@@ -227,19 +227,82 @@ def _drop_scales(blk, lay, device):
     return tuple(dp.sample(lens.numel(), device).repeat_interleave(lens, output_size=lay.T) for _ in range(2))
 
 
-def _branch_out(inp, lin, resid, scale):
+class DropCfg:
+    """Dropout of one block call (modules.py): the attention probabilities' (SDPA dropout_p =
+    proj_drop_prob, applied whether or not the module trains, :246 / 370 / 417; without SDPA, attn_drop
+    while training, :252 / 376 / 423), the projection's proj_drop (:257 / 381) and the MLP's two
+    nn.Dropout (after the activation and after fc2, :75-82) while training. Each active one gets its own
+    seed for vj_common.h's mask hash, kept for the backward. SwiGLUFFN takes no dropout (its `drop` is
+    unused in the reference too)."""
+
+    def __init__(self, attn=None, mlp=None):
+        self.pa, self.pp = _attn_drop_probs(attn) if attn is not None else (0.0, 0.0)
+        self.pm = _mlp_drop_prob(mlp) if mlp is not None else 0.0
+        self.sa, self.sp, self.sm1, self.sm2 = (_drop_seed() if p > 0 else 0 for p in (self.pa, self.pp, self.pm,
+                                                                                        self.pm))
+
+    @property
+    def branches(self):  # proj / MLP dropout: the residual adds leave the GEMM epilogues
+        return self.pp > 0 or self.pm > 0
+
+
+def _attn_drop_probs(attn):
+    """(attention-probability dropout, proj_drop) in effect for a call of `attn` (see DropCfg)."""
+    if getattr(attn, "use_sdpa", True):
+        pa = float(getattr(attn, "proj_drop_prob", 0.0) or 0.0)
+    else:
+        pa = float(attn.attn_drop.p) if attn.attn_drop.training else 0.0
+    pp = float(attn.proj_drop.p) if attn.proj_drop.training else 0.0
+    return pa, pp
+
+
+def _mlp_drop_prob(mlp):
+    drop = None if getattr(mlp, "swiglu", False) else getattr(mlp, "drop", None)
+    return float(drop.p) if drop is not None and drop.training else 0.0
+
+
+def _has_dropout(blk):
+    return any(_attn_drop_probs(blk.attn)) or _mlp_drop_prob(blk.mlp) > 0
+
+
+def _drop_seed():
+    """A 32-bit mask seed from torch's (CPU) default generator: torch.manual_seed makes runs replay."""
+    return int(torch.randint(0, 2**32, (1,), dtype=torch.int64))
+
+
+def _drop_cfg(blk):
+    return DropCfg(blk.attn, blk.mlp) if _has_dropout(blk) else None
+
+
+def _branch_out(inp, lin, resid, scale, p=0.0, seed=0):
     """resid + lin(inp): the residual add of a branch, fused into the output GEMM's epilogue; with a
-    drop_path factor the GEMM writes the branch and vj_rowscale_add scales and adds it."""
-    if scale is None:
+    drop_path factor the GEMM writes the branch and vj_rowscale_add scales and adds it; with dropout
+    (p > 0) vj_dropout drops the branch (then drop_path, if any) and adds it."""
+    if scale is None and p == 0:
         return ops.linear_fwd(inp, weight_bf16(lin.weight), lin.bias, _resid_epi(resid), resid=resid)
-    return ops.rowscale_add(ops.linear_fwd(inp, weight_bf16(lin.weight), lin.bias, EPI_F32), scale, resid)
+    y = ops.linear_fwd(inp, weight_bf16(lin.weight), lin.bias, EPI_F32)
+    if p == 0:
+        return ops.rowscale_add(y, scale, resid)
+    if scale is None:
+        return ops.dropout(y, p, seed, resid=resid)
+    return ops.rowscale_add(ops.dropout(y, p, seed).float(), scale, resid)
 
 
-def _mlp_forward(ln2, mlp, save):
+def _branch_grad(dxo, scale, p, seed):
+    """bf16 gradient of a branch's output projection from the residual stream's gradient: drop_path's
+    factor, then dropout's mask (the forward applied them in the other order)."""
+    g = ops.rowscale_bf16(dxo, scale) if scale is not None else dxo
+    if p > 0:
+        return ops.dropout(g, p, seed)
+    return g if g.dtype == BF16 else ops.cast_bf16(g)
+
+
+def _mlp_forward(ln2, mlp, save, p=0.0, seed=0):
     """The MLP up to its output projection: (that projection's input, the output Linear, saved).
     GELU MLP (modules.py:77-83): fc1 + GELU in one GEMM epilogue, which also saves GELU'(pre-activation)
-    for the backward (bf16, the bytes the pre-activation took). SwiGLUFFN (modules.py:102-106): fc1 and
-    fc2 write x1 | x2 side by side, vj_swiglu_fwd makes silu(x1) * x2."""
+    for the backward (bf16, the bytes the pre-activation took), then the activation's dropout (p > 0).
+    SwiGLUFFN (modules.py:102-106): fc1 and fc2 write x1 | x2 side by side, vj_swiglu_fwd makes
+    silu(x1) * x2."""
     T = ln2.shape[0]
     if getattr(mlp, "swiglu", False):
         h = mlp.fc1.weight.shape[0]
@@ -250,6 +313,8 @@ def _mlp_forward(ln2, mlp, save):
         return hidden, mlp.fc3, ((x12, hidden) if save else None)
     dgelu = torch.empty(T, mlp.fc1.weight.shape[0], dtype=BF16, device=ln2.device) if save else None
     _, act = ops.linear_fwd(ln2, weight_bf16(mlp.fc1.weight), mlp.fc1.bias, EPI_GELU, out=dgelu)
+    if p > 0:
+        act = ops.dropout(act, p, seed)
     return act, mlp.fc2, ((dgelu, act) if save else None)
 
 
@@ -265,6 +330,8 @@ def block_forward(x, blk, lay, save):
     scales = _drop_scales(blk, lay, x.device)
     if save and scales is not None and x.dtype == BF16:
         raise NotImplementedError("drop_path on the trained bf16 residual stream (the trainer keeps f32 there)")
+    dc = _drop_cfg(blk)
+    pa, sa = (dc.pa, dc.sa) if dc is not None else (0.0, 0)
     ln1, m1, r1 = ops.layernorm_fwd(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, want_stats=save)
     if attn.use_rope:  # QKV GEMM with RoPE of q, k fused into its epilogue
         c, s = rope_tables(hd, x.device, lay.npos)
@@ -272,12 +339,12 @@ def block_forward(x, blk, lay, save):
                            lay.tpr, c, s)
     else:
         qkv = ops.linear_fwd(ln1, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
-    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd, lay), fblk=lay.fblk)
-    x_mid = _branch_out(o, attn.proj, x, scales and scales[0])
+    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd, lay), fblk=lay.fblk, dropout_p=pa, seed=sa)
+    x_mid = _branch_out(o, attn.proj, x, scales and scales[0], *((dc.pp, dc.sp) if dc else ()))
     ln2, m2, r2 = ops.layernorm_fwd(x_mid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, want_stats=save)
-    hidden, out_lin, msaved = _mlp_forward(ln2, mlp, save)
-    x_out = _branch_out(hidden, out_lin, x_mid, scales and scales[1])
-    saved = (x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, msaved, scales) if save else None
+    hidden, out_lin, msaved = _mlp_forward(ln2, mlp, save, *((dc.pm, dc.sm1) if dc else ()))
+    x_out = _branch_out(hidden, out_lin, x_mid, scales and scales[1], *((dc.pm, dc.sm2) if dc else ()))
+    saved = (x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, msaved, scales, dc) if save else None
     return x_out, saved
 
 
@@ -286,8 +353,8 @@ def block_forward_f32(x, blk, lay):
     (vj_gemm_f32) and exact-softmax attention (vj_attn_fwd_f32); every intermediate stays f32."""
     if lay.fblk:
         raise NotImplementedError("the fp32-operand parity mode has no frame-causal attention")
-    if getattr(blk.mlp, "swiglu", False) or _drop_scales(blk, lay, x.device) is not None:
-        raise NotImplementedError("the fp32-operand parity mode covers the GELU MLP without drop_path")
+    if getattr(blk.mlp, "swiglu", False) or _drop_scales(blk, lay, x.device) is not None or _has_dropout(blk):
+        raise NotImplementedError("the fp32-operand parity mode covers the GELU MLP without drop_path / dropout")
     attn, mlp = blk.attn, blk.mlp
     H = attn.num_heads
     hd = x.shape[1] // H
@@ -455,7 +522,7 @@ def _ln_grads(ln):
     return grad_buf(ln.weight), grad_buf(ln.bias)
 
 
-def _mlp_backward(dy_b, mlp, ln2, saved):
+def _mlp_backward(dy_b, mlp, ln2, saved, p=0.0, seed=0):
     """bf16 gradient of the MLP output -> bf16 gradient of its input ln2; weight and hidden-bias
     gradients accumulated (the output Linear's bias gradient is the caller's). Each weight gradient is
     issued before the data gradient that shares its dY, so on the weight-gradient stream the two overlap.
@@ -479,7 +546,11 @@ def _mlp_backward(dy_b, mlp, ln2, saved):
     dgelu, act = saved
     with _OnWgradStream(dy_b, act):
         wgrad(dy_b, act, mlp.fc2.weight)
-    dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
+    if p > 0:  # the activation's dropout between the fc2 data gradient and GELU's backward
+        dh = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), wt=weight_bf16_t(mlp.fc2.weight))
+        dpre = ops.dropout(dh, p, seed, aux=dgelu)
+    else:
+        dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
     with _OnWgradStream(dpre, ln2):
         wgrad(dpre, ln2, mlp.fc1.weight)
         _bias_grad(mlp.fc1, dpre)
@@ -487,13 +558,17 @@ def _mlp_backward(dy_b, mlp, ln2, saved):
 
 
 def block_backward(dxo, blk, lay, saved):
-    x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, msaved, scales = saved
+    x, ln1, m1, r1, qkv, o, stats, x_mid, ln2, m2, r2, msaved, scales, dc = saved
+    branch_drop = dc is not None and dc.branches
     attn, mlp = blk.attn, blk.mlp
     out_lin = mlp.fc3 if getattr(mlp, "swiglu", False) else mlp.fc2
     T, D = x.shape
     H = attn.num_heads
     hd = D // H
-    if dxo.dtype == BF16:  # bf16 residual stream: its gradient is bf16 too (as under the reference's autocast)
+    if branch_drop:  # dropout (and drop_path) of the MLP branch: the bias gradient from its dY, not from dxo
+        dy_mlp = _branch_grad(dxo, scales and scales[1], dc.pm, dc.sm2)
+        _bias_grad(out_lin, dy_mlp)
+    elif dxo.dtype == BF16:  # bf16 residual stream: its gradient is bf16 too (as under the reference's autocast)
         dy_mlp = dxo
     elif scales is None:
         twin = getattr(dxo, "_vj_grad_bf16", None)  # bf16 twin written by the next block's LN1 backward,
@@ -501,16 +576,16 @@ def block_backward(dxo, blk, lay, saved):
     else:  # drop_path: the MLP branch's dY = its factor x dxo (bias gradient from it, not from dxo)
         dy_mlp = ops.rowscale_bf16(dxo, scales[1])
         _bias_grad(out_lin, dy_mlp)
-    dln2 = _mlp_backward(dy_mlp, mlp, ln2, msaved)
+    dln2 = _mlp_backward(dy_mlp, mlp, ln2, msaved, *((dc.pm, dc.sm1) if dc else ()))
     gw, gb = _ln_grads(blk.norm2)
-    # without drop_path the output-projection / proj bias gradients are the column sums of dxo / dxm,
-    # fused into the LayerNorm backward
-    fused = scales is None
+    # without drop_path / dropout the output-projection / proj bias gradients are the column sums of
+    # dxo / dxm, fused into the LayerNorm backward
+    fused = scales is None and not branch_drop
     dxm, dxm_b = ops.layernorm_bwd(dln2, x_mid, m2, r2, blk.norm2.weight, dres_in=dxo, dweight=gw, dbias=gb,
                                    want_bf16=fused, sum_in=_bias_buf(out_lin) if fused else None,
                                    sum_out=_bias_buf(attn.proj) if fused else None)
     if not fused:
-        dxm_b = ops.rowscale_bf16(dxm, scales[0])
+        dxm_b = _branch_grad(dxm, scales and scales[0], dc.pp if dc else 0.0, dc.sp if dc else 0)
         _bias_grad(attn.proj, dxm_b)
     # attention
     with _OnWgradStream(dxm_b, o):
@@ -520,7 +595,8 @@ def block_backward(dxo, blk, lay, saved):
     if attn.use_rope:  # inverse RoPE fused into the dq / dk stores of the attention backward
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
-    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk,
+                        dropout_p=dc.pa if dc else 0.0, seed=dc.sa if dc else 0)
     with _OnWgradStream(dqkv, ln1):
         wgrad(dqkv, ln1, attn.qkv.weight)
         _bias_grad(attn.qkv, dqkv)
@@ -584,15 +660,21 @@ def attn_module_forward(x, attn, lay):
                            lay.tpr, c, s)
     else:
         qkv = ops.linear_fwd(x, weight_bf16(attn.qkv.weight), attn.qkv.bias, EPI_BF16)
-    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd, lay), fblk=lay.fblk)
+    dc = DropCfg(attn=attn) if any(_attn_drop_probs(attn)) else None
+    o, stats = ops.attn_fwd(qkv, H, hd, lay.groups, _attn_scale(attn, hd, lay), fblk=lay.fblk,
+                            dropout_p=dc.pa if dc else 0.0, seed=dc.sa if dc else 0)
     y = ops.linear_fwd(o, weight_bf16(attn.proj.weight), attn.proj.bias, EPI_F32)
-    return y, (x, qkv, o, stats)
+    if dc is not None and dc.pp > 0:  # proj_drop (modules.py:257 / 381): the module's output in bf16
+        y = ops.dropout(y, dc.pp, dc.sp).float()
+    return y, (x, qkv, o, stats, dc)
 
 
 def attn_module_backward(dy, attn, lay, saved):
-    x, qkv, o, stats = saved
+    x, qkv, o, stats, dc = saved
     H = attn.num_heads
     hd = x.shape[1] // H
+    if dc is not None and dc.pp > 0:
+        dy = ops.dropout(dy, dc.pp, dc.sp).float()
     dy_b = ops.cast_bf16(dy)
     do = ops.linear_dgrad(dy_b, weight_bf16(attn.proj.weight), wt=weight_bf16_t(attn.proj.weight))
     wgrad(dy_b, o, attn.proj.weight)
@@ -601,7 +683,8 @@ def attn_module_backward(dy, attn, lay, saved):
     if attn.use_rope:
         c, s = rope_tables(hd, x.device, lay.npos)
         rope = (lay.ids, lay.ids_mod, lay.tpf, lay.tpr, c, s)
-    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk)
+    dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk,
+                        dropout_p=dc.pa if dc else 0.0, seed=dc.sa if dc else 0)
     dx = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
     wgrad(dqkv, x, attn.qkv.weight)
     _bias_grad(attn.qkv, dqkv)
@@ -610,14 +693,19 @@ def attn_module_backward(dy, attn, lay, saved):
 
 def mlp_module_forward(x, mlp):
     """x bf16 [T, C] -> (fc2(GELU(fc1 x)) or SwiGLU's fc3(silu(fc1 x) * fc2 x), f32; saved)."""
-    hidden, out_lin, msaved = _mlp_forward(x, mlp, True)
+    dc = DropCfg(mlp=mlp) if _mlp_drop_prob(mlp) > 0 else None
+    hidden, out_lin, msaved = _mlp_forward(x, mlp, True, *((dc.pm, dc.sm1) if dc else ()))
     y = ops.linear_fwd(hidden, weight_bf16(out_lin.weight), out_lin.bias, EPI_F32)
-    return y, (x, msaved)
+    if dc is not None:  # the output dropout (modules.py:82)
+        y = ops.dropout(y, dc.pm, dc.sm2).float()
+    return y, (x, msaved, dc)
 
 
 def mlp_module_backward(dy, mlp, saved):
-    x, msaved = saved
-    dx = _mlp_backward(ops.cast_bf16(dy), mlp, x, msaved)
+    x, msaved, dc = saved
+    if dc is not None:
+        dy = ops.dropout(dy, dc.pm, dc.sm2).float()
+    dx = _mlp_backward(ops.cast_bf16(dy), mlp, x, msaved, *((dc.pm, dc.sm1) if dc else ()))
     _bias_grad(mlp.fc3 if getattr(mlp, "swiglu", False) else mlp.fc2, dy)
     return dx
 

@@ -15,7 +15,8 @@ from . import ops
 
 
 class MLP(nn.Module):
-    """modules.py:67-83 (fc1 -> GELU(erf) -> fc2; dropout p=0)."""
+    """modules.py:67-83 (fc1 -> GELU(erf) -> dropout -> fc2 -> dropout; the two nn.Dropout run while
+    training, on vj_dropout's element masks)."""
 
     def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.0):
         super().__init__()
@@ -27,8 +28,6 @@ class MLP(nn.Module):
         self.drop = nn.Dropout(drop)
         if act_layer is not nn.GELU:
             raise NotImplementedError("MLP supports the exact-erf GELU (nn.GELU) on the HIP path")
-        if drop:
-            raise NotImplementedError("MLP dropout > 0 is not implemented (configs use 0)")
 
     def forward(self, x):
         """modules.py:77-83: fc2(GELU(fc1(x))), fc1 + GELU fused in one GEMM epilogue."""
@@ -157,10 +156,13 @@ class Attention(nn.Module):
 
 
 def _check_attn(head_dim, attn_drop, proj_drop, is_causal):
+    """Dropout: proj_drop is also SDPA's dropout_p (modules.py:246 / 370 / 417, active in eval too, as
+    there); attn_drop only acts without SDPA (use_sdpa=False, while training). Both run on the kernels'
+    hash masks (vj_attn_fwd_ex, vj_dropout)."""
     if head_dim not in (32, 64, 80, 88):
         raise NotImplementedError(f"HIP attention supports head_dim 32, 64, 80, 88 (got {head_dim})")
-    if attn_drop or proj_drop:
-        raise NotImplementedError("attention/projection dropout > 0 is not implemented (configs use 0)")
+    if not (0.0 <= attn_drop < 1.0 and 0.0 <= proj_drop < 1.0):
+        raise ValueError(f"dropout probabilities must be in [0, 1) (attn_drop={attn_drop}, proj_drop={proj_drop})")
     if is_causal:
         raise NotImplementedError("causal attention is not on the V-JEPA pre-training path")
 

@@ -460,9 +460,10 @@ def rope_(qkv, H, hd, q_off, k_off, ids, ids_mod, tpf, tpr, cos_tab, sin_tab, in
          _p(cos_tab), _p(sin_tab), half, int(inverse), _stream())
 
 
-def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None, fblk=0):
+def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None, fblk=0, dropout_p=0.0, seed=0):
     """groups: list of (nseq, len). Returns (O bf16 [T, H*hd], stats f32 [2, H, T]). fblk > 0: frame-causal
-    mask (token i sees key j iff j // fblk <= i // fblk)."""
+    mask (token i sees key j iff j // fblk <= i // fblk). dropout_p > 0: SDPA's attention dropout with the
+    mask of `seed` (vj_attn_fwd_ex; the backward needs the same p and seed)."""
     _dev(qkv)
     T = qkv.shape[0]
     D = H * hd
@@ -472,26 +473,48 @@ def attn_fwd(qkv, H, hd, groups, scale, q_off=None, k_off=None, v_off=None, fblk
     o = torch.empty(T, D, dtype=BF16, device=qkv.device)
     stats = torch.empty(2, H, T, dtype=F32, device=qkv.device)
     ns, ln = [g[0] for g in groups], [g[1] for g in groups]
-    _call("vj_attn_fwd_fc", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, v_off, _p(o), D, _p(stats),
-          float(scale), len(groups), int_array(ns), int_array(ln), int(fblk), _stream(),
+    _call("vj_attn_fwd_ex", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), q_off, k_off, v_off, _p(o), D, _p(stats),
+          float(scale), len(groups), int_array(ns), int_array(ln), int(fblk), float(dropout_p), int(seed) & 0xFFFFFFFF,
+          _stream(),
           label=f"attn_fwd<hd{hd}>", flops=sum(4.0 * n * l * l * D for n, l in groups))
     return o, stats
 
 
-def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None, fblk=0):
-    """rope = (ids, ids_mod, tpf, tpr, cos_tab, sin_tab) -> dq, dk returned w.r.t. the un-rotated q, k."""
+def attn_bwd(qkv, o, do, stats, H, hd, groups, scale, dqkv=None, rope=None, fblk=0, dropout_p=0.0, seed=0):
+    """rope = (ids, ids_mod, tpf, tpr, cos_tab, sin_tab) -> dq, dk returned w.r.t. the un-rotated q, k.
+    dropout_p, seed: those of the forward (attention dropout)."""
     _dev(qkv, o, do, stats)
     T = qkv.shape[0]
     D = H * hd
     dqkv = dqkv if dqkv is not None else torch.empty(T, 3 * D, dtype=BF16, device=qkv.device)
     ns, ln = [g[0] for g in groups], [g[1] for g in groups]
     ids, mod, tpf, tpr, ct, st = rope if rope is not None else (None, 0, 0, 0, None, None)
-    _call("vj_attn_bwd_fc", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
+    _call("vj_attn_bwd_ex", T, H, hd, _p(qkv), _rowmajor(qkv, "qkv"), 0, D, 2 * D, _p(o), _rowmajor(o, "o"), _p(do),
           _rowmajor(do, "do"), _p(stats), _p(dqkv), _rowmajor(dqkv, "dqkv"), float(scale), len(groups), int_array(ns),
-          int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), int(fblk), _stream(),
-          label=f"attn_bwd<hd{hd}>",
+          int_array(ln), _p(ids), int(mod), int(tpf), int(tpr), _p(ct), _p(st), int(fblk), float(dropout_p),
+          int(seed) & 0xFFFFFFFF, _stream(), label=f"attn_bwd<hd{hd}>",
           flops=sum(10.0 * n * l * l * D for n, l in groups))  # FA2 convention: 5 matmuls = 2.5 x forward
     return dqkv
+
+
+def dropout(x, p, seed, resid=None, aux=None, out=None):
+    """nn.Dropout's forward (or, on a gradient with the forward's seed, its backward) on a row-major
+    [M, N] tensor (vj_dropout): bf16(bf16(x) * z), z = 1 / (1 - p) on kept elements. x f32 or bf16;
+    resid (f32 / bf16): returns resid + that, in resid's dtype; aux (bf16): returns bf16(that * aux)."""
+    _dev(x)
+    M, N = x.shape
+    if resid is not None:
+        assert resid.shape == x.shape and resid.dtype in (F32, BF16)
+        out = out if out is not None else torch.empty(M, N, dtype=resid.dtype, device=x.device)
+    else:
+        out = out if out is not None else torch.empty(M, N, dtype=BF16, device=x.device)
+    if aux is not None:
+        assert aux.shape == x.shape and aux.dtype == BF16
+    _call("vj_dropout", M, N, _p(x), _rowmajor(x, "x"), int(x.dtype == F32), _p(aux),
+          _rowmajor(aux, "aux") if aux is not None else 0, _p(resid), _rowmajor(resid, "resid") if resid is not None else 0,
+          int(resid is not None and resid.dtype == F32), _p(out), _rowmajor(out, "out"), float(p), int(seed) & 0xFFFFFFFF,
+          _stream(), label="vj_dropout")
+    return out
 
 
 def _xattn_ws(B, nq, N, H, hd, device):

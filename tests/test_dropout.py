@@ -92,14 +92,18 @@ def test_dropout_kernel_bit_exact(mode, x_f32):
     assert torch.equal(out.float().cpu(), exp), (out.float().cpu() - exp).abs().max()
 
 
-def _attn_drop_ref(q, k, v, groups, scale, H, p, seed):
+def _attn_drop_ref(q, k, v, groups, scale, H, p, seed, fblk=0):
     """fp32 attention with the kernels' dropout mask: O = (softmax(S) * Z) V, Z[t, h, j] = keep / (1 - p)
-    for query token t, head h, key j of its sequence (mask row t * H + h, column j)."""
+    for query token t, head h, key j of its sequence (mask row t * H + h, column j); fblk > 0 adds the
+    frame-causal mask (key j visible to query i iff j // fblk <= i // fblk, modules.py:12-23)."""
     outs, t0 = [], 0
     for ns, ln in groups:
         for _ in range(ns):
             qq, kk, vv = (x[t0:t0 + ln].transpose(0, 1) for x in (q, k, v))
             s = (qq @ kk.transpose(-1, -2)) * scale
+            if fblk:
+                f = torch.arange(ln) // fblk
+                s = s.masked_fill(f[None, :] > f[:, None], float("-inf"))
             rows = (np.arange(t0, t0 + ln)[None, :] * H + np.arange(H)[:, None]).reshape(-1)
             z = torch.from_numpy(vj_dropout_mask_ref(seed, rows, np.arange(ln), p)).float().reshape(H, ln, ln)
             outs.append(((torch.softmax(s, -1) * z / (1 - p)) @ vv).transpose(0, 1))
@@ -108,9 +112,11 @@ def _attn_drop_ref(q, k, v, groups, scale, H, p, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hd,H,groups", [(64, 2, [(3, 70), (2, 130)]), (32, 3, [(2, 257), (1, 5)]),
-                                         (32, 2, [(1, 1504)]), (88, 2, [(1, 200), (3, 31)])])
-def test_attention_dropout_fwd_bwd(hd, H, groups):
+@pytest.mark.parametrize("hd,H,groups,fblk", [(64, 2, [(3, 70), (2, 130)], 0), (32, 3, [(2, 257), (1, 5)], 0),
+                                              (32, 2, [(1, 1504)], 0), (88, 2, [(1, 200), (3, 31)], 0),
+                                              # frame-causal (the action-conditioned predictor), partial last frame
+                                              (64, 2, [(1, 500), (2, 70)], 130)])
+def test_attention_dropout_fwd_bwd(hd, H, groups, fblk):
     """Attention dropout (vj_attn_fwd_ex / vj_attn_bwd_ex) vs fp32 autograd on the same mask; the
     statistics (lse) are those of the undropped scores; deterministic for a seed."""
     from vjepa2_amd import ops
@@ -121,22 +127,23 @@ def test_attention_dropout_fwd_bwd(hd, H, groups):
     g = torch.Generator().manual_seed(hd + T)
     qkv = torch.randn(T, 3 * D, generator=g).to(DEV).bfloat16()
     scale = hd ** -0.5
-    o, stats = ops.attn_fwd(qkv, H, hd, groups, scale, dropout_p=p, seed=seed)
-    o0, stats0 = ops.attn_fwd(qkv, H, hd, groups, scale)
+    o, stats = ops.attn_fwd(qkv, H, hd, groups, scale, dropout_p=p, seed=seed, fblk=fblk)
+    o0, stats0 = ops.attn_fwd(qkv, H, hd, groups, scale, fblk=fblk)
     q, k, v = (qkv[:, i * D:(i + 1) * D].float().cpu().reshape(T, H, hd).requires_grad_(True) for i in range(3))
-    o_ref = _attn_drop_ref(q, k, v, groups, scale, H, p, seed)
+    o_ref = _attn_drop_ref(q, k, v, groups, scale, H, p, seed, fblk)
     torch.cuda.synchronize()
     rel = lambda a, b: ((a.float().cpu() - b.float()).norm() / b.float().norm()).item()  # noqa: E731
     assert rel(o.reshape(T, H, hd), o_ref.detach()) < 1e-2
     assert torch.equal(stats[0], stats0[0])  # log-sum-exp of the undropped scores
     do = torch.randn(T, D, generator=g).bfloat16()
     o_ref.backward(do.float().reshape(T, H, hd))
-    dqkv = ops.attn_bwd(qkv, o, do.to(DEV), stats, H, hd, groups, scale, dropout_p=p, seed=seed)
+    dqkv = ops.attn_bwd(qkv, o, do.to(DEV), stats, H, hd, groups, scale, dropout_p=p, seed=seed, fblk=fblk)
     torch.cuda.synchronize()
     for i, (name, t) in enumerate((("dq", q), ("dk", k), ("dv", v))):
         r = rel(dqkv[:, i * D:(i + 1) * D].reshape(T, H, hd), t.grad)
         assert r < 2e-2, (name, r)
-    assert torch.equal(dqkv, ops.attn_bwd(qkv, o, do.to(DEV), stats, H, hd, groups, scale, dropout_p=p, seed=seed))
+    assert torch.equal(dqkv, ops.attn_bwd(qkv, o, do.to(DEV), stats, H, hd, groups, scale, dropout_p=p, seed=seed,
+                                          fblk=fblk))
 
 
 @pytest.mark.gpu

@@ -266,7 +266,10 @@ def _has_dropout(blk):
 
 
 def _drop_seed():
-    """A 32-bit mask seed from torch's (CPU) default generator: torch.manual_seed makes runs replay."""
+    """A 32-bit mask seed from torch's default CPU generator, so torch.manual_seed replays a run. Only
+    blocks with an active dropout draw (the shipped configs never do); the reference's dropout draws
+    from the CUDA generator instead, so with dropout on, later CPU draws of this process (e.g. masks
+    made in the main process) follow another sequence than the reference's."""
     return int(torch.randint(0, 2**32, (1,), dtype=torch.int64))
 
 

@@ -59,6 +59,14 @@ int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, con
 int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
                         int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
                         void* C2, long ldc2, int splitk, float* ws, long ws_floats, void* stream);
+/* nn.Linear's weight AND bias gradients from one read of dY (the autograd of F.linear, modules.py:77-83,
+ * 330, 379-381): dw[M, N] (+)= dY^T X (accumulate), db[M] (+)= sum_k dY[k, m] (db_accumulate; db may be
+ * NULL), dY [K, M] and X [K, N] row-major bf16 (K = tokens), split-K as vj_gemm_bf16_splitk. The bias sums
+ * are fused into the split-K GEMM's 256-row kernel (f32, fixed order) when it runs, else computed by a
+ * column-sum pass. ws >= max(splitk > 1 ? splitk * (M * N + M) : 0, min(256, ceil(K / 64)) * M) floats. */
+int vj_gemm_bf16_wgrad(int M, int N, int K, const void* dy, long lddy, const void* x, long ldx, float* dw, long lddw,
+                       int accumulate, float* db, int db_accumulate, int splitk, float* ws, long ws_floats,
+                       void* stream);
 
 /* Varlen non-causal flash attention, head_dim 32, 64, 80 or 88 (80 / 88 padded to 96 in LDS and in the
  * MFMA loops; F.scaled_dot_product_attention,

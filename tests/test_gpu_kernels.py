@@ -87,7 +87,33 @@ def test_gemm_splitk(epi, MNK):
     assert torch.equal(out, first), "split-K must be deterministic"
 
 
-@pytest.mark.parametrize("N", [256, 384, 200, 1152])
+@pytest.mark.parametrize("NKM", [(1024, 1024, 11712), (4096, 1024, 5000), (1152, 384, 3000), (1032, 1408, 2000),
+                                 (384, 1152, 71232), (200, 136, 3000), (1024, 1024, 700), (12, 64, 999)])
+@pytest.mark.parametrize("acc", [False, True])
+def test_wgrad_fused_bias(NKM, acc):
+    """vj_gemm_bf16_wgrad: dW (+)= dY^T X and db (+)= dY.sum(0) in one call (nn.Linear's weight and bias
+    gradients). Split-K shapes with M >= 256 sum the bias inside the 256-row partial kernel (column tile
+    0's A fragments; ragged M = 1032 / 1152, BN = 128 for N = 384, 256-wide N = 1408); the rest (128-tile
+    kernel, no split, a 12-wide output) take the column-sum pass. Against float64 sums of the same bf16
+    values; deterministic."""
+    from vjepa2_amd import ops
+
+    N, K, M = NKM
+    g = torch.Generator(device="cpu").manual_seed(N + K + M)
+    dY = torch.randn(M, N, generator=g).to(DEV).bfloat16()
+    X = torch.randn(M, K, generator=g).to(DEV).bfloat16()
+    dw0, db0 = torch.randn(N, K, generator=g).to(DEV), torch.randn(N, generator=g).to(DEV)
+    exp_w = dY.double().t() @ X.double() + (dw0.double() if acc else 0)
+    exp_b = dY.double().sum(0) + db0.double()  # db always accumulates (grad_buf semantics)
+    outs = []
+    for _ in range(2):
+        dw, db = dw0.clone(), db0.clone()
+        ops.linear_wgrad(dY, X, dw, accumulate=acc, db=db)
+        outs.append((dw, db))
+    torch.cuda.synchronize()
+    _close(outs[0][0], exp_w, 2e-4 * math.sqrt(M), 1e-5, f"wgrad dW {NKM}")
+    _close(outs[0][1], exp_b, 2e-5 * math.sqrt(M), 1e-5, f"wgrad db {NKM}")
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), "must be deterministic"
 @pytest.mark.parametrize("M", [333, 1333])
 def test_gemm_epilogues(M, N):
     """Every epilogue; M >= 1024 runs the 256-row kernel (N = 256: 256-wide tiles, 384 / 200: 128-wide,

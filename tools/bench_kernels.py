@@ -60,6 +60,12 @@ GEMMS = [
     ("wgrad fc1", 4096, 1024, 11712, 0, 0, 2, 4),
     ("wgrad qkv", 3072, 1024, 11712, 0, 0, 2, 5),
     ("wgrad proj", 1024, 1024, 11712, 0, 0, 2, 15),
+    # 9: weight + bias gradient (vj_gemm_bf16_wgrad: the bias sums fused; a library without it runs
+    # the split-K GEMM + vj_colsum_f32, the pre-fusion path)
+    ("wgrad+b fc1", 4096, 1024, 11712, 0, 0, 9, 4),
+    ("wgrad+b qkv", 3072, 1024, 11712, 0, 0, 9, 5),
+    ("pred wgrad+b fc1", 1536, 384, 71232, 0, 0, 9, 14),
+    ("pred wgrad+b qkv", 1152, 384, 71232, 0, 0, 9, 14),
     # ViT-g (D = 1408) weight gradients, K = 34304 context tokens: split 4 / 5 / 6 (the 128- and
     # 256-wide column-tile sizings pick different splits)
     ("g wgrad qkv s4", 4224, 1408, 34304, 0, 0, 2, 4),
@@ -95,6 +101,8 @@ ATTN = [("attn fwd hd64 ctx", 64, 16, [(24, 424), (24, 64)], False),
 
 def gemm_case(lib, case, dev, stream):
     name, M, N, K, akm, bkm, epi, sk = case
+    rowsum = epi == 9
+    epi = 2 if rowsum else epi
     save_d = epi == 7
     epi = 3 if save_d else (7 if epi == 8 else epi)  # 8: EPI_BF16_RESID (7 in the library)
     g = torch.Generator(device="cpu").manual_seed(0)
@@ -111,6 +119,21 @@ def gemm_case(lib, case, dev, stream):
     aux = C if epi in (2, 7) else ((torch.rand(M, N, generator=g) * 4 - 2).to(dev).bfloat16() if epi == 4 else None)
     ws = torch.empty(max(1, sk * M * N if sk > 1 else 1), device=dev)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    if rowsum:
+        db = torch.zeros(M, device=dev)
+        ws = torch.empty(max(sk * (M * N + M), 256 * M), device=dev)
+        fused = hasattr(lib, "vj_gemm_bf16_wgrad")
+
+        def run_rs():
+            if fused:
+                rc = lib.vj_gemm_bf16_wgrad(M, N, K, p(A), lda, p(B), ldb, p(C), N, 1, p(db), 1, sk, p(ws), ws.numel(),
+                                            stream)
+            else:
+                rc = lib.vj_gemm_bf16_splitk(M, N, K, p(A), lda, akm, p(B), ldb, bkm, 2, None, p(C), N, p(C), N, None, 0,
+                                             sk, p(ws), ws.numel(), stream)
+                rc = rc or lib.vj_colsum_f32(K, M, p(A), 1, lda, p(db), 1, p(ws), ws.numel(), stream)
+            assert rc == 0, rc
+        return run_rs, 2.0 * M * N * K
 
     def run():
         rc = lib.vj_gemm_bf16_splitk(M, N, K, p(A), lda, akm, p(B), ldb, bkm, epi, p(bias), p(aux), N if aux is not None else 0,
@@ -201,6 +224,21 @@ def ln_bwd_case(lib, M, D, acc, dev, stream):
     nb = lib.vj_layernorm_bwd_blocks(M)
     ws = torch.empty(nb * 2 * D, device=dev)
     p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    if rowsum:
+        db = torch.zeros(M, device=dev)
+        ws = torch.empty(max(sk * (M * N + M), 256 * M), device=dev)
+        fused = hasattr(lib, "vj_gemm_bf16_wgrad")
+
+        def run_rs():
+            if fused:
+                rc = lib.vj_gemm_bf16_wgrad(M, N, K, p(A), lda, p(B), ldb, p(C), N, 1, p(db), 1, sk, p(ws), ws.numel(),
+                                            stream)
+            else:
+                rc = lib.vj_gemm_bf16_splitk(M, N, K, p(A), lda, akm, p(B), ldb, bkm, 2, None, p(C), N, p(C), N, None, 0,
+                                             sk, p(ws), ws.numel(), stream)
+                rc = rc or lib.vj_colsum_f32(K, M, p(A), 1, lda, p(db), 1, p(ws), ws.numel(), stream)
+            assert rc == 0, rc
+        return run_rs, 2.0 * M * N * K
 
     def run():
         rc = lib.vj_layernorm_bwd(M, D, p(dy), D, p(x), D, p(mean), p(rstd), p(gamma), p(dres_in), D, p(dres), D,

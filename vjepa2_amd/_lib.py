@@ -27,6 +27,7 @@ SIGNATURES = {
     "vj_device_sync": [],
     "vj_gemm_bf16": [_I, _I, _I, _P, _L, _I, _P, _L, _I, _I, _P, _P, _L, _P, _L, _P, _L, _P],
     "vj_gemm_bf16_splitk": [_I, _I, _I, _P, _L, _I, _P, _L, _I, _I, _P, _P, _L, _P, _L, _P, _L, _I, _P, _L, _P],
+    "vj_gemm_bf16_wgrad": [_I, _I, _I, _P, _L, _P, _L, _P, _L, _I, _P, _I, _I, _P, _L, _P],
     "vj_attn_fwd": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _F, _I, _P, _P, _P],
     "vj_attn_bwd": [_I, _I, _I, _P, _L, _I, _I, _I, _P, _L, _P, _L, _P, _P, _L, _F, _I, _P, _P, _P, _I, _I, _I, _P,
                     _P, _P],

@@ -167,9 +167,10 @@ __device__ __forceinline__ uint32_t f8pack4(float a, float b, float c, float d) 
 
 // GEMM epilogues: ONE numbering for every GEMM source (vj_gemm.hip, vj_gemm256.hip, vj_gemm_pp.hip,
 // vj_f32.hip) and the public header (include/vjepa_hip.h VJ_EPI_*). EPI_PARTIAL is internal (split-K
-// f32 partial slabs); EPI_BF16_RESID: bf16 residual in (aux), bf16 out.
+// f32 partial slabs), and so is EPI_PARTIAL_RS (the same with A's row sums per K slice: the fused
+// bias gradient of vj_gemm_bf16_wgrad); EPI_BF16_RESID: bf16 residual in (aux), bf16 out.
 enum { EPI_BF16 = 0, EPI_F32 = 1, EPI_F32_RESID = 2, EPI_GELU = 3, EPI_GELU_BWD = 4, EPI_ROPE = 5, EPI_PARTIAL = 6,
-       EPI_BF16_RESID = 7 };
+       EPI_BF16_RESID = 7, EPI_PARTIAL_RS = 8 };
 
 static inline int vj_cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 

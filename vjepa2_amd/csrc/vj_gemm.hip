@@ -39,6 +39,10 @@ struct GemmArgs {
   long ldaux;
   int kslice;  // split-K: K range of blockIdx.z is [z*kslice, min(K, (z+1)*kslice))
   float* ws;   // EPI_PARTIAL: f32 partial tiles [splitk][M][N]
+  // split-K reduce only: rs_out[m] (+)= sum_z rs_ws[z][m] (the fused bias gradient of vj_gemm_bf16_wgrad)
+  const float* rs_ws = nullptr;
+  float* rs_out = nullptr;
+  int rs_acc = 0;
 };
 
 constexpr int BM = 128, BN = 128, BK = 64;
@@ -195,12 +199,20 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   }
 }
 
+// the fused row sums (bias gradient) of row m, by the thread of the row's first columns: fixed z order
+__device__ __forceinline__ void reduce_rowsum(const GemmArgs& g, int splitk, int m) {
+  float s = 0.f;
+  for (int z = 0; z < splitk; ++z) s += g.rs_ws[(long)z * g.M + m];
+  g.rs_out[m] = g.rs_acc ? g.rs_out[m] + s : s;
+}
+
 // Split-K combine, 4 columns per thread (N % 4 == 0): C = epilogue(sum_z ws[z]) in fixed z order.
 __global__ void k_splitk_reduce4(GemmArgs g, int splitk, int epi) {
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   const long total = (long)g.M * g.N;
   if (i >= total) return;
   const int m = (int)(i / g.N), n = (int)(i % g.N);
+  if (g.rs_out && n == 0) reduce_rowsum(g, splitk, m);
   float4 v = g.bias ? *(const float4*)(g.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int z = 0; z < splitk; ++z) {
     const float4 w = *(const float4*)(g.ws + (long)z * total + i);
@@ -222,6 +234,7 @@ __global__ void k_splitk_reduce(GemmArgs g, int splitk, int epi) {
   const long total = (long)g.M * g.N;
   if (i >= total) return;
   const int m = (int)(i / g.N), n = (int)(i % g.N);
+  if (g.rs_out && n == 0) reduce_rowsum(g, splitk, m);
   float v = g.bias ? g.bias[n] : 0.f;
   for (int z = 0; z < splitk; ++z) v += g.ws[(long)z * total + i];
   if (epi == EPI_F32_RESID) {
@@ -252,15 +265,19 @@ int launch_epi(int epi, const GemmArgs& g, dim3 grid, hipStream_t st) {
 }  // namespace
 
 int vj_gemm256_partial(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
-                       int b_kmajor, int kslice, int splitk, float* ws, hipStream_t st);
+                       int b_kmajor, int kslice, int splitk, float* ws, hipStream_t st, float* rsum);
 int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
                         int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
                         void* C2, long ldc2, hipStream_t st, const void* rope);
 
-extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B,
-                                   long ldb, int b_kmajor, int epi, const float* bias, const void* aux, long ldaux,
-                                   void* C, long ldc, void* C2, long ldc2, int splitk, float* ws, long ws_floats,
-                                   void* stream) {
+// The split-K GEMM. rs_out (or null): also rs_out[m] (+= if rs_acc) = sum_k A[m, k], fused into the
+// 256-row partial kernel when that runs (*rs_done = 1; ws then holds splitk * (M * N + M) floats),
+// else left to the caller (*rs_done = 0).
+static int gemm_splitk(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
+                       int b_kmajor, int epi, const float* bias, const void* aux, long ldaux, void* C, long ldc,
+                       void* C2, long ldc2, int splitk, float* ws, long ws_floats, void* stream, float* rs_out,
+                       int rs_acc, int* rs_done) {
+  if (rs_done) *rs_done = 0;
   if (M == 0 || N == 0) return VJ_OK;
   VJ_CHECK_ARG(M > 0 && N > 0 && K > 0, "vj_gemm_bf16: bad dims M=%d N=%d K=%d", M, N, K);
   VJ_CHECK_ARG(epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID || epi == EPI_GELU || epi == EPI_GELU_BWD ||
@@ -303,7 +320,15 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
   }
   if (splitk > 1) {
     int rc = VJ_ERR_UNSUPPORTED;
-    rc = vj_gemm256_partial(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, kslice, splitk, ws, st);
+    const bool rs = rs_out && ws_floats >= (long)splitk * M * N + (long)splitk * M;
+    rc = vj_gemm256_partial(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, kslice, splitk, ws, st,
+                            rs ? ws + (long)splitk * M * N : nullptr);
+    if (rc == VJ_OK && rs) {
+      g.rs_ws = ws + (long)splitk * M * N;
+      g.rs_out = rs_out;
+      g.rs_acc = rs_acc;
+      if (rs_done) *rs_done = 1;
+    }
     if (rc == VJ_ERR_UNSUPPORTED) {
       if (a_kmajor && b_kmajor) rc = launch_epi<true, true>(EPI_PARTIAL, g, grid, st);
       else if (a_kmajor && !b_kmajor) rc = launch_epi<true, false>(EPI_PARTIAL, g, grid, st);
@@ -325,6 +350,33 @@ extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda,
   if (a_kmajor && !b_kmajor) return launch_epi<true, false>(epi, g, grid, st);
   if (!a_kmajor && b_kmajor) return launch_epi<false, true>(epi, g, grid, st);
   return launch_epi<false, false>(epi, g, grid, st);
+}
+
+extern "C" int vj_gemm_bf16_splitk(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B,
+                                   long ldb, int b_kmajor, int epi, const float* bias, const void* aux, long ldaux,
+                                   void* C, long ldc, void* C2, long ldc2, int splitk, float* ws, long ws_floats,
+                                   void* stream) {
+  return gemm_splitk(M, N, K, A, lda, a_kmajor, B, ldb, b_kmajor, epi, bias, aux, ldaux, C, ldc, C2, ldc2, splitk, ws,
+                     ws_floats, stream, nullptr, 0, nullptr);
+}
+
+extern "C" int vj_colsum_f32(int M, int N, const void* x, int x_bf16, long ld, float* out, int accumulate, float* ws,
+                             long ws_floats, void* stream);
+
+// nn.Linear's weight and bias gradients from one read of dY: dw[M, N] (+)= dY^T X and db[M] (+)=
+// dY.sum(0), with dY [K, M] and X [K, N] row-major (K = tokens). Split-K as vj_gemm_bf16_splitk;
+// the bias sums ride in the 256-row partial kernel (v_dot2 of the dY fragments it already holds)
+// when it runs, else a column-sum pass follows (same results up to f32 summation order).
+extern "C" int vj_gemm_bf16_wgrad(int M, int N, int K, const void* dy, long lddy, const void* x, long ldx,
+                                  float* dw, long lddw, int accumulate, float* db, int db_accumulate, int splitk,
+                                  float* ws, long ws_floats, void* stream) {
+  VJ_CHECK_ARG(dw, "vj_gemm_bf16_wgrad: null dw");
+  int done = 0;
+  const int rc = gemm_splitk(M, N, K, dy, lddy, 0, x, ldx, 0, accumulate ? EPI_F32_RESID : EPI_F32, nullptr,
+                             accumulate ? dw : nullptr, lddw, dw, lddw, nullptr, 0, splitk, ws, ws_floats, stream, db,
+                             db_accumulate, &done);
+  if (rc || !db || done || M == 0) return rc;
+  return vj_colsum_f32(K, M, dy, 1, lddy, db, db_accumulate, ws, ws_floats, stream);
 }
 
 extern "C" int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,

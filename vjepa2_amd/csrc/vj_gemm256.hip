@@ -82,9 +82,10 @@ __device__ __forceinline__ void vm_wait() {
 #endif
 template <bool AK, bool BKM, int EPI, int BN, bool F8 = false, int NWV = 8, int BMT = 256, int STG = 0>
 __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
-  static_assert(!STG || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256 && EPI != EPI_PARTIAL),
+  constexpr bool PART = EPI == EPI_PARTIAL || EPI == EPI_PARTIAL_RS;  // split-K partial slabs (RS: + row sums)
+  static_assert(!STG || (AK && BKM && !F8 && NWV == 8 && BMT == 256 && BN == 256 && !PART),
                 "staggered main loop: 8-wave K-major bf16 256 x 256 tiles");
-  static_assert(!F8 || (AK && BKM && EPI != EPI_PARTIAL && EPI != EPI_GELU_BWD), "fp8: forward GEMMs only");
+  static_assert(!F8 || (AK && BKM && !PART && EPI != EPI_GELU_BWD), "fp8: forward GEMMs only");
   static_assert(NWV == 8 || (NWV == 4 && AK && BKM && !F8), "2-workgroup GEMM: K-major bf16 operands only");
   constexpr int BM = BMT;
   constexpr int MH = BM / 64;     // virtual 16-row m-tiles per half of the wave's rows (4 / 3)
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
   static_assert(BMT == 256 || (BMT == 192 && !F8 && AK && DIRECT && (NWV == 8 || EPI != EPI_ROPE)),
                 "192-row tiles: direct K-major bf16 (the 4-wave kernel without the RoPE table)");
   constexpr bool AUX = EPI == EPI_F32_RESID || EPI == EPI_GELU_BWD || EPI == EPI_BF16_RESID;
-  constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_F32_RESID || EPI == EPI_PARTIAL;
+  constexpr bool F32OUT = EPI == EPI_F32 || EPI == EPI_F32_RESID || PART;
 
   // The next tile's stage 0 is DMA'd during this tile's last K-tile. Its stage 1 goes out right
   // after the last barrier, unless the epilogue still needs that LDS slot (staged epilogue: after
@@ -446,12 +447,42 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         acc[2 * qq + i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(X[i], Y8[j], acc[2 * qq + i][j], 0, 0,
                                                                               0, f8sa[2 * qq + i], 0, f8sb[j]);
   };
+  // Fused bias gradient (EPI_PARTIAL_RS, tiles of column tile 0): row sums of the A
+  // fragments the MFMAs already hold. Wave (wr, wc) sums m-tiles 2 wc and 2 wc + 1 of its 128-row
+  // band (so the 4 waves of a band cover its 8 m-tiles once), in M-half wc / 2, with v_dot2 against
+  // bf16 ones: 4 VALU per m-tile and k-step beside 16 MFMAs, two f32 registers per lane (lane l:
+  // row l & 15, k = 8 (l >> 4) .. + 7; the 4 lane groups are summed in the epilogue).
+  constexpr bool RS = EPI == EPI_PARTIAL_RS;
+  [[maybe_unused]] float rsa = 0.f, rsb = 0.f;
+  [[maybe_unused]] bool rs_on = false;
+  auto rsum8 = [](const bf16x8& x, float s) {
+    typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+    const bf16x2_t one = {(__bf16)1.0f, (__bf16)1.0f};
+    s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 0, 1), one, s, false);
+    s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 2, 3), one, s, false);
+    s = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 4, 5), one, s, false);
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(x, x, 6, 7), one, s, false);
+  };
+  auto rs_phase = [&](const bf16x8 (&X)[MH], int mh) {
+    if constexpr (RS && MH == 4) {
+      if (rs_on && (wc >> 1) == mh) {  // wave-uniform
+        if (wc & 1) {
+          rsa = rsum8(X[2], rsa);
+          rsb = rsum8(X[3], rsb);
+        } else {
+          rsa = rsum8(X[0], rsa);
+          rsb = rsum8(X[1], rsb);
+        }
+      }
+    }
+  };
   auto mm = [&](const bf16x8 (&X)[MH], int mh, const bf16x8 (&Y)[NTN]) {
 #pragma unroll
     for (int i = 0; i < MH; ++i)
 #pragma unroll
       for (int j = 0; j < NTN; ++j)
         acc[mh * MH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * MH + i][j], 0, 0, 0);
+    rs_phase(X, mh);
   };
   // m-tiles i0 .. i1 - 1 of one phase (the last phase is split around the B DMA pieces)
   auto mm_rows = [&](const bf16x8 (&X)[MH], int mh, const bf16x8 (&Y)[NTN], int i0, int i1) {
@@ -461,6 +492,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
 #pragma unroll
         for (int j = 0; j < NTN; ++j)
           acc[mh * MH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(X[i], Y[j], acc[mh * MH + i][j], 0, 0, 0);
+    if (i1 == MH) rs_phase(X, mh);
   };
   // MN-major operands are read with asm transposed reads (ds_read_tr16_async): each phase first
   // waits for the fragments it consumes (read in the previous phase), then issues the next reads.
@@ -496,6 +528,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
     for (int i = 0; i < 2 * MH; ++i)
 #pragma unroll
       for (int j = 0; j < NTN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (RS) {
+      rs_on = g.rsum && cur.n0 == 0;
+      rsa = rsb = 0.f;
+    }
     if constexpr (F8) {  // this tile's per-row scale exponents (retired by the wait below)
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -862,7 +898,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       float bias[NTN];
 #pragma unroll
       for (int j = 0; j < NTN; ++j) bias[j] = STG ? biasp[j] : 0.f;
-      if (!STG && EPI != EPI_GELU_BWD && EPI != EPI_PARTIAL && g.bias && nok)
+      if (!STG && EPI != EPI_GELU_BWD && !PART && g.bias && nok)
 #pragma unroll
         for (int j = 0; j < NTN; ++j) bias[j] = g.bias[nb + j];
       // RoPE (modules.py:26-50, 343-365): tile rows' (frame, row, col) positions + interleaved
@@ -953,10 +989,10 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       // per-tile lane offsets of the bf16 outputs (C, C2) and the f32 output rows
       [[maybe_unused]] const long off_c = (long)mrow * g.ldc + nb8;
       [[maybe_unused]] const long off_c2 = EPI == EPI_GELU ? (long)mrow * g.ldc2 + nb8 : 0;
-      [[maybe_unused]] const long off_f = EPI == EPI_PARTIAL ? ((long)cur.z * g.M + mb) * g.N + nb
+      [[maybe_unused]] const long off_f = PART ? ((long)cur.z * g.M + mb) * g.N + nb
                                                              : (long)mb * g.ldc + nb;
-      [[maybe_unused]] const long ld_f = EPI == EPI_PARTIAL ? (long)g.N : g.ldc;
-      [[maybe_unused]] float* const base_f = EPI == EPI_PARTIAL ? g.ws : (float*)g.C;
+      [[maybe_unused]] const long ld_f = PART ? (long)g.N : g.ldc;
+      [[maybe_unused]] float* const base_f = PART ? g.ws : (float*)g.C;
       if constexpr (AUX)
 #pragma unroll
         for (int i = 0; i < AUX_PF; ++i) {
@@ -1088,6 +1124,15 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
       constexpr int IT = PR / RPI;   // row-instructions per pass
       static_assert(8 * PR * STR * 4 <= STAGE, "staging image must fit one operand slot");
       LDS_AS float* wl = (LDS_AS float*)(smem + sle * STAGE + wave * PR * STR * 4);
+      if constexpr (RS && MH == 4) {
+        if (rs_on) {  // the row sums: lane groups (k sub-ranges) added, rows 32 wc + 16 (lane >> 4) + (lane & 15)
+          float sa = rsa + __shfl_xor(rsa, 16), sb = rsb + __shfl_xor(rsb, 16);
+          sa += __shfl_xor(sa, 32);
+          sb += __shfl_xor(sb, 32);
+          const int m = cur.m0 + wr * 128 + 32 * wc + (lane & 31);
+          if (lane < 32 && m < g.M) g.rsum[(long)cur.z * g.M + m] = lane < 16 ? sa : sb;
+        }
+      }
       bool ract[2] = {false, false};
       int rsh[2] = {0, 0}, rf0[2] = {0, 0}, rf1[2] = {0, 0};
       const int col = (lane % LPR) * 4;  // this thread's 4 columns, fixed for every row it stores
@@ -1111,7 +1156,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
         __syncthreads();
       }
       float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (EPI != EPI_GELU_BWD && EPI != EPI_PARTIAL && g.bias && ncol < g.N) bias4 = *(const float4*)(g.bias + ncol);
+      if (EPI != EPI_GELU_BWD && !PART && g.bias && ncol < g.N) bias4 = *(const float4*)(g.bias + ncol);
 #pragma unroll
       for (int pass = 0; pass < 8 / MTP; ++pass) {
 #pragma unroll
@@ -1161,7 +1206,7 @@ __global__ __launch_bounds__(NWV * 64, 2) void k_gemm256(G256 g) {
             *(uint2*)((bf16_t*)g.C + (long)m * g.ldc + n) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
           } else if constexpr (EPI == EPI_F32) {
             *(float4*)((float*)g.C + (long)m * g.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
-          } else if constexpr (EPI == EPI_PARTIAL) {
+          } else if constexpr (PART) {
             *(float4*)(g.ws + ((long)cur.z * g.M + m) * g.N + n) = make_float4(v[0], v[1], v[2], v[3]);
           } else if constexpr (EPI == EPI_F32_RESID) {
             const float4 rr = rres[it];
@@ -1448,6 +1493,13 @@ int launch256(int epi, const G256& g, hipStream_t st) {
       } else {
         return VJ_ERR_UNSUPPORTED;
       }
+    case EPI_PARTIAL_RS:  // the same with the fused bias gradient (g.rsum)
+      if constexpr (!AK && !BKM) {
+        hipLaunchKernelGGL((k_gemm256<AK, BKM, EPI_PARTIAL_RS, BN>), grid, dim3(512), 0, st, g);
+        break;
+      } else {
+        return VJ_ERR_UNSUPPORTED;
+      }
     default: vj_set_error("gemm256: bad epilogue %d", epi); return VJ_ERR_ARG;
   }
   VJ_LAUNCH_CHECK("vj_gemm256");
@@ -1519,9 +1571,10 @@ int vj_gemm256_dispatch(int M, int N, int K, const void* A, long lda, int a_kmaj
 }
 
 // Split-K partial products ws[z] = A[:, z-th K slice] B[z-th K slice, :]^T (f32, [splitk][M][N]) with
-// 256-row tiles; the caller reduces the slabs. Returns VJ_ERR_UNSUPPORTED when it declines.
+// 256-row tiles; the caller reduces the slabs. rsum (or null): the row sums of A per K slice,
+// [splitk][M] (fused bias gradient). Returns VJ_ERR_UNSUPPORTED when it declines.
 int vj_gemm256_partial(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,
-                       int b_kmajor, int kslice, int splitk, float* ws, hipStream_t st) {
+                       int b_kmajor, int kslice, int splitk, float* ws, hipStream_t st, float* rsum) {
   if (a_kmajor || b_kmajor || N % 8 || M < 256 || N < 128) return VJ_ERR_UNSUPPORTED;
   // 256-wide tiles unless the last one would waste more than 15 % of the columns (the forward GEMMs'
   // rule): ViT-g's N = 1408 runs 6 tiles of 256 instead of 11 of 128 (twice the work per operand byte)
@@ -1530,8 +1583,9 @@ int vj_gemm256_partial(int M, int N, int K, const void* A, long lda, int a_kmajo
   if ((long)tm * tn * splitk > 0x7fffffffL) return VJ_ERR_UNSUPPORTED;
   G256 g{(const bf16_t*)A, (const bf16_t*)B, M, N, K, lda, ldb, nullptr, 0, nullptr, 0, nullptr, nullptr, 0,
          tm, tn, RopeP{}, kslice, splitk, ws, tile_group(tm, tn)};
-  return bn == 256 ? launch256<false, false, 256>(EPI_PARTIAL, g, st)
-                   : launch256<false, false, 128>(EPI_PARTIAL, g, st);
+  g.rsum = rsum;
+  const int epi = rsum ? EPI_PARTIAL_RS : EPI_PARTIAL;
+  return bn == 256 ? launch256<false, false, 256>(epi, g, st) : launch256<false, false, 128>(epi, g, st);
 }
 
 extern "C" int vj_gemm_bf16(int M, int N, int K, const void* A, long lda, int a_kmajor, const void* B, long ldb,

@@ -35,6 +35,9 @@ struct G256 {
   // scales: A(m, k) = a8 * 2^ea[m], B(n, k) = b8 * 2^eb[n] (E8M0 scale operands of the MFMA)
   const int* ea = nullptr;
   const int* eb = nullptr;
+  // EPI_PARTIAL: f32 row sums of A over each K slice, [nsplit][M] (the bias gradient fused into a
+  // weight-gradient GEMM: A = dY^T, so row m of A summed over the tokens is db[m]); null: none
+  float* rsum = nullptr;
 };
 
 constexpr int BK = 64;

@@ -126,10 +126,12 @@ def wgrad_buf(p):
     return p.grad, True
 
 
-def wgrad(dy, x, w, shape=None):
-    """dW (+)= dY^T X into w's gradient (nn.Linear / Conv3d-as-GEMM weight gradient)."""
+def wgrad(dy, x, w, shape=None, lin=None):
+    """dW (+)= dY^T X into w's gradient (nn.Linear / Conv3d-as-GEMM weight gradient); with `lin` (the
+    Linear owning w) its bias gradient dY.sum(0) too, summed inside the same GEMM."""
     buf, acc = wgrad_buf(w)
-    ops.linear_wgrad(dy, x, buf if shape is None else buf.view(*shape), accumulate=acc)
+    db = _bias_buf(lin) if lin is not None else None
+    ops.linear_wgrad(dy, x, buf if shape is None else buf.view(*shape), accumulate=acc, db=db)
 
 
 _ROPE_TABLES = {}
@@ -540,10 +542,8 @@ def _mlp_backward(dy_b, mlp, ln2, saved, p=0.0, seed=0):
         dx12 = ops.swiglu_bwd(dh, x12)
         dx1, dx2 = dx12[:, :h], dx12[:, h:]
         with _OnWgradStream(dx12, ln2):
-            wgrad(dx1, ln2, mlp.fc1.weight)
-            _bias_grad(mlp.fc1, dx1)
-            wgrad(dx2, ln2, mlp.fc2.weight)
-            _bias_grad(mlp.fc2, dx2)
+            wgrad(dx1, ln2, mlp.fc1.weight, lin=mlp.fc1)
+            wgrad(dx2, ln2, mlp.fc2.weight, lin=mlp.fc2)
         dl = ops.linear_dgrad(dx1, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
         return ops.linear_dgrad(dx2, weight_bf16(mlp.fc2.weight), wt=weight_bf16_t(mlp.fc2.weight), resid=dl)
     dgelu, act = saved
@@ -555,8 +555,7 @@ def _mlp_backward(dy_b, mlp, ln2, saved, p=0.0, seed=0):
     else:
         dpre = ops.linear_dgrad(dy_b, weight_bf16(mlp.fc2.weight), gelu_grad=dgelu, wt=weight_bf16_t(mlp.fc2.weight))
     with _OnWgradStream(dpre, ln2):
-        wgrad(dpre, ln2, mlp.fc1.weight)
-        _bias_grad(mlp.fc1, dpre)
+        wgrad(dpre, ln2, mlp.fc1.weight, lin=mlp.fc1)
     return ops.linear_dgrad(dpre, weight_bf16(mlp.fc1.weight), wt=weight_bf16_t(mlp.fc1.weight))
 
 
@@ -601,8 +600,7 @@ def block_backward(dxo, blk, lay, saved):
     dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk,
                         dropout_p=dc.pa if dc else 0.0, seed=dc.sa if dc else 0)
     with _OnWgradStream(dqkv, ln1):
-        wgrad(dqkv, ln1, attn.qkv.weight)
-        _bias_grad(attn.qkv, dqkv)
+        wgrad(dqkv, ln1, attn.qkv.weight, lin=attn.qkv)
     dln1 = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
     gw, gb = _ln_grads(blk.norm1)
     dxi, dxi_b = ops.layernorm_bwd(dln1, x, m1, r1, blk.norm1.weight, dres_in=dxm, dweight=gw, dbias=gb,
@@ -689,8 +687,7 @@ def attn_module_backward(dy, attn, lay, saved):
     dqkv = ops.attn_bwd(qkv, o, do, stats, H, hd, lay.groups, _attn_scale(attn, hd, lay), rope=rope, fblk=lay.fblk,
                         dropout_p=dc.pa if dc else 0.0, seed=dc.sa if dc else 0)
     dx = ops.linear_dgrad(dqkv, weight_bf16(attn.qkv.weight), wt=weight_bf16_t(attn.qkv.weight))
-    wgrad(dqkv, x, attn.qkv.weight)
-    _bias_grad(attn.qkv, dqkv)
+    wgrad(dqkv, x, attn.qkv.weight, lin=attn.qkv)
     return dx
 
 

@@ -19,6 +19,8 @@ F32 = torch.float32
 
 
 _SHAPE_LABELS = bool(int(__import__("os").environ.get("VJ_SHAPE_LABELS", "0")))
+# A/B knob: VJ_WGRAD_BIAS=0 computes the bias gradients by a separate column-sum pass (the pre-round-6 path)
+_WGRAD_BIAS = os.environ.get("VJ_WGRAD_BIAS", "1") != "0"
 
 
 class KernelEvents:
@@ -93,10 +95,7 @@ def gemm(M, N, K, a, lda, a_kmajor, b, ldb, b_kmajor, epi, out=None, ldc=0, out2
     label = f"k_gemm<{int(a_kmajor)},{int(b_kmajor)},{EPI_NAMES[epi]}>"
     if _SHAPE_LABELS:  # diagnostics (VJ_SHAPE_LABELS=1): per-shape kernel-event labels
         label += f"[{M}x{N}x{K}]"
-    if splitk > 1:  # same slicing as the library: kslice = ceil(ceil(K / splitk) / 64) * 64
-        kslice = (K + splitk - 1) // splitk
-        kslice = (kslice + 63) // 64 * 64
-        splitk = (K + kslice - 1) // kslice
+    splitk = _effective_splitk(K, splitk)
     if splitk > 1:
         ws = torch.empty(splitk * M * N, dtype=F32, device=a.device)
         _call("vj_gemm_bf16_splitk", M, N, K, _p(a), lda, int(a_kmajor), _p(b), ldb, int(b_kmajor), epi, _p(bias),
@@ -105,6 +104,15 @@ def gemm(M, N, K, a, lda, a_kmajor, b, ldb, b_kmajor, epi, out=None, ldc=0, out2
         return
     _call("vj_gemm_bf16", M, N, K, _p(a), lda, int(a_kmajor), _p(b), ldb, int(b_kmajor), epi, _p(bias), _p(aux), ldaux,
           _p(out), ldc, _p(out2), ldc2, _stream(), label=label, flops=2.0 * M * N * K)
+
+
+def _effective_splitk(K, splitk):
+    """The library's slicing: kslice = ceil(ceil(K / splitk) / 64) * 64, splitk = ceil(K / kslice)."""
+    if splitk <= 1:
+        return 1
+    kslice = (K + splitk - 1) // splitk
+    kslice = (kslice + 63) // 64 * 64
+    return (K + kslice - 1) // kslice
 
 
 def wgrad_splitk(M, N, K, cus=None):
@@ -246,11 +254,26 @@ def _pad_rows(t):
     return out
 
 
-def linear_wgrad(dy, x, dw, accumulate=True):
-    """dW[N,K] += dY^T X  (f32 accumulate into dw); accumulate=False: dW = dY^T X (overwrite)."""
+def linear_wgrad(dy, x, dw, accumulate=True, db=None):
+    """dW[N,K] += dY^T X  (f32 accumulate into dw); accumulate=False: dW = dY^T X (overwrite).
+    db (f32 [N] or None): db += dY.sum(0), the bias gradient, from the same GEMM (vj_gemm_bf16_wgrad)."""
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M and dw.shape == (N, K) and dw.dtype == F32
+    if db is not None and (N % 8 or K % 8 or not _WGRAD_BIAS):
+        linear_wgrad(dy, x, dw, accumulate)
+        return colsum(dy, db)
+    if db is not None:
+        _dev(dy, x, dw, db)
+        assert db.dtype == F32 and db.numel() == N and db.is_contiguous()
+        s = wgrad_splitk(N, K, M)
+        s = _effective_splitk(M, s)
+        nws = max(s * (N * K + N) if s > 1 else 0, min(256, max(1, (M + 63) // 64)) * N)
+        ws = torch.empty(nws, dtype=F32, device=dy.device)
+        _call("vj_gemm_bf16_wgrad", N, K, M, _p(dy), _rowmajor(dy, "dy"), _p(x), _rowmajor(x, "x"), _p(dw),
+              _rowmajor(dw, "dw"), int(accumulate), _p(db), 1, s, _p(ws), ws.numel(), _stream(),
+              label="k_gemm<0,0,wgrad+bias>", flops=2.0 * M * N * K)
+        return dw
     if N % 8:  # dY^T is the MN-major A operand: its contiguous dim N must be a multiple of 8
         tmp = torch.zeros((N + 7) // 8 * 8, K, dtype=F32, device=dw.device)
         linear_wgrad(_pad_cols(dy), x, tmp)

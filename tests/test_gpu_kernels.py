@@ -114,6 +114,9 @@ def test_wgrad_fused_bias(NKM, acc):
     _close(outs[0][0], exp_w, 2e-4 * math.sqrt(M), 1e-5, f"wgrad dW {NKM}")
     _close(outs[0][1], exp_b, 2e-5 * math.sqrt(M), 1e-5, f"wgrad db {NKM}")
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), "must be deterministic"
+
+
+@pytest.mark.parametrize("N", [256, 384, 200, 1152])
 @pytest.mark.parametrize("M", [333, 1333])
 def test_gemm_epilogues(M, N):
     """Every epilogue; M >= 1024 runs the 256-row kernel (N = 256: 256-wide tiles, 384 / 200: 128-wide,

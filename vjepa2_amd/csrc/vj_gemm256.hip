@@ -1516,7 +1516,12 @@ extern "C" int vj_set_reserved_cus(int n) {
 
 // 256-wide column tiles unless the last one would waste more than 15 % of the work (measured,
 // tools/bench_kernels.py: predictor QKV N = 1152 -17 % with 256-wide tiles; N = 384 +14 %)
-bool wide_tile_ok(int N) { return N % 256 == 0 || (N > 256 && vj_cdiv(N, 256) * 256L * 100 <= 115L * N); }
+#ifndef VJ_WIDE_ALL
+#define VJ_WIDE_ALL 0  // variant builds: 256-wide column tiles for every N > 256
+#endif
+bool wide_tile_ok(int N) {
+  return N % 256 == 0 || (N > 256 && (VJ_WIDE_ALL || vj_cdiv(N, 256) * 256L * 100 <= 115L * N));
+}
 
 // Called by vj_gemm_bf16_splitk (splitk == 1) when the problem suits a 256-row tile; arguments
 // already validated there. Returns VJ_ERR_UNSUPPORTED when it declines.

@@ -57,9 +57,12 @@ def test_library_metadata_and_errors():
     # argument validation happens before any device work -> usable without a GPU
     rc = lib.vj_gemm_bf16(16, 16, 12, None, 16, 1, None, 16, 1, 0, None, None, 0, None, 16, None, 0, None)
     assert rc != 0 and "null operand" in _lib.last_error()
-    for internal in (5, 6):  # RoPE / split-K partial epilogues are internal: rejected at the C ABI
+    for internal in (5, 6, 8):  # RoPE / split-K partial (+ row sums) epilogues are internal: rejected at the C ABI
         rc = lib.vj_gemm_bf16(16, 16, 16, None, 16, 1, None, 16, 1, internal, None, None, 0, None, 16, None, 0, None)
         assert rc != 0 and "not a public epilogue" in _lib.last_error()
+    # the fused weight + bias gradient validates before any launch
+    rc = lib.vj_gemm_bf16_wgrad(64, 64, 64, None, 64, None, 64, None, 64, 0, None, 0, 1, None, 0, None)
+    assert rc != 0 and "null dw" in _lib.last_error()
     rc = lib.vj_attn_fwd(10, 2, 48, None, 288, 0, 96, 192, None, 96, None, 0.1, 1, _lib.int_array([1]),
                          _lib.int_array([10]), None)
     assert rc != 0 and "head_dim" in _lib.last_error()
